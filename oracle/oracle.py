@@ -1,0 +1,165 @@
+"""ctypes wrapper for the CPU oracle (oracle/gbcore.c). TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module;
+the product path (pokegym_amd) never does.  See gbcore.h for what the oracle restates and its
+parity status (PPU/savestate pinned on the reference's 264 savestates; CPU trajectories vs
+PyBoy unpinned).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libgbcore.so")
+STATE_SIZE = 142610
+ROWS, COLS = 144, 160
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        L.gb_new.restype = ctypes.c_void_p
+        L.gb_new.argtypes = [u8p, ctypes.c_uint32]
+        L.gb_free.argtypes = [ctypes.c_void_p]
+        L.gb_clone.restype = ctypes.c_void_p
+        L.gb_clone.argtypes = [ctypes.c_void_p]
+        L.gb_power_on.argtypes = [ctypes.c_void_p]
+        L.gb_load_state.argtypes = [ctypes.c_void_p, u8p, ctypes.c_uint32]
+        L.gb_save_state.argtypes = [ctypes.c_void_p, u8p, ctypes.c_uint32]
+        L.gb_button.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.gb_set_rendering.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.gb_tick.argtypes = [ctypes.c_void_p]
+        L.gb_run_action.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.gb_read.restype = ctypes.c_uint8
+        L.gb_read.argtypes = [ctypes.c_void_p, ctypes.c_uint16]
+        L.gb_write.argtypes = [ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint8]
+        L.gb_screen_shades.restype = u8p
+        L.gb_screen_shades.argtypes = [ctypes.c_void_p]
+        L.gb_wram.restype = u8p
+        L.gb_wram.argtypes = [ctypes.c_void_p]
+        L.gb_instr_count.restype = ctypes.c_uint64
+        L.gb_instr_count.argtypes = [ctypes.c_void_p]
+        L.gb_frame_count.restype = ctypes.c_uint64
+        L.gb_frame_count.argtypes = [ctypes.c_void_p]
+        L.gb_crashed.argtypes = [ctypes.c_void_p]
+        L.gb_render_from_state.argtypes = [u8p, ctypes.c_uint32, u8p]
+        L.gb_batch_run.argtypes = [u8p, ctypes.c_uint32, u8p, ctypes.c_uint32, ctypes.c_uint32,
+                                   ctypes.c_uint32, u8p, ctypes.c_int, u8p, u8p]
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+def render_from_state(state: bytes) -> np.ndarray:
+    """PPU restatement: render 144x160 shade ids from a v9 state's VRAM/OAM/regs/line params."""
+    s = np.frombuffer(state, dtype=np.uint8).copy()
+    out = np.zeros((ROWS, COLS), np.uint8)
+    rc = lib().gb_render_from_state(_ptr(s), len(s), _ptr(out))
+    if rc:
+        raise ValueError(f"gb_render_from_state failed: {rc}")
+    return out
+
+
+class GB:
+    """One oracle emulator (PyBoy-1.x-shaped)."""
+
+    def __init__(self, rom: bytes, state: bytes | None = None, _handle=None):
+        self._rom = np.frombuffer(rom, dtype=np.uint8).copy()  # keep alive: gbcore borrows it
+        L = lib()
+        self.h = _handle if _handle is not None else L.gb_new(_ptr(self._rom), len(self._rom))
+        if not self.h:
+            raise ValueError("unsupported ROM (size/MBC)")
+        if state is not None:
+            self.load_state(state)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().gb_free(self.h)
+            self.h = None
+
+    def clone(self) -> "GB":
+        g = GB.__new__(GB)
+        g._rom = self._rom
+        g.h = lib().gb_clone(self.h)
+        return g
+
+    def load_state(self, state: bytes):
+        s = np.frombuffer(state, dtype=np.uint8).copy()
+        if lib().gb_load_state(self.h, _ptr(s), len(s)):
+            raise ValueError("bad v9 savestate")
+
+    def save_state(self) -> bytes:
+        out = np.zeros(STATE_SIZE, np.uint8)
+        lib().gb_save_state(self.h, _ptr(out), STATE_SIZE)
+        return out.tobytes()
+
+    def power_on(self):
+        lib().gb_power_on(self.h)
+
+    def tick(self):
+        lib().gb_tick(self.h)
+
+    def button(self, b: int, pressed: bool):
+        lib().gb_button(self.h, b, 1 if pressed else 0)
+
+    def set_rendering(self, on: bool):
+        lib().gb_set_rendering(self.h, 1 if on else 0)
+
+    def run_action(self, action: int, frame_skip: int = 24, release_frame: int = 8):
+        lib().gb_run_action(self.h, int(action), frame_skip, release_frame)
+
+    def read(self, addr: int) -> int:
+        return lib().gb_read(self.h, addr)
+
+    def write(self, addr: int, v: int):
+        lib().gb_write(self.h, addr, v)
+
+    def screen(self) -> np.ndarray:
+        p = lib().gb_screen_shades(self.h)
+        return np.ctypeslib.as_array(p, shape=(ROWS, COLS)).copy()
+
+    def wram(self) -> np.ndarray:
+        p = lib().gb_wram(self.h)
+        return np.ctypeslib.as_array(p, shape=(8192,)).copy()
+
+    @property
+    def instr_count(self) -> int:
+        return lib().gb_instr_count(self.h)
+
+    @property
+    def crashed(self) -> bool:
+        return bool(lib().gb_crashed(self.h))
+
+
+def batch_run(rom: bytes, state: bytes | None, actions: np.ndarray, want_states=True, want_screens=True):
+    """Run n envs x steps env-steps; actions shape (steps, n) uint8. Returns (states, screens)."""
+    actions = np.ascontiguousarray(actions, dtype=np.uint8)
+    steps, n = actions.shape
+    r = np.frombuffer(rom, dtype=np.uint8).copy()
+    st = np.frombuffer(state, dtype=np.uint8).copy() if state is not None else None
+    so = np.zeros((n, STATE_SIZE), np.uint8) if want_states else None
+    sc = np.zeros((n, ROWS, COLS), np.uint8) if want_screens else None
+    rc = lib().gb_batch_run(_ptr(r), len(r), _ptr(st) if st is not None else None,
+                            len(st) if st is not None else 0, n, steps, _ptr(actions), 1,
+                            _ptr(so) if so is not None else None, _ptr(sc) if sc is not None else None)
+    if rc:
+        raise ValueError(f"gb_batch_run failed: {rc}")
+    return so, sc

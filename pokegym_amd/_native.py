@@ -1,0 +1,79 @@
+"""ctypes binding of the C ABI in include/pokegym_amd.h (libpokegym_amd.so, built in-tree).
+
+This is the reference-side binding a maintainer would add.  There is no
+CPU fallback: if the HIP library is missing or fails to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libpokegym_amd.so")
+
+PK_F_RENDER = 1
+STATE_V9_BYTES = 142610
+ROWS, COLS = 144, 160
+
+# the exported symbols declared in include/pokegym_amd.h
+EXPORTS = ("pk_create", "pk_destroy", "pk_last_error", "pk_abi_version", "pk_reset", "pk_step",
+           "pk_screen_ptr", "pk_num_envs", "pk_peek", "pk_poke", "pk_snapshot", "pk_load_env",
+           "pk_last_instr_count")
+
+
+class PkConfig(ctypes.Structure):
+    _fields_ = [
+        ("n_envs", ctypes.c_uint32),
+        ("device", ctypes.c_int32),
+        ("rom", ctypes.POINTER(ctypes.c_uint8)),
+        ("rom_len", ctypes.c_uint64),
+        ("state", ctypes.POINTER(ctypes.c_uint8)),
+        ("state_len", ctypes.c_uint64),
+        ("frame_skip", ctypes.c_uint32),
+        ("release_frame", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32),
+        ("max_episode_steps", ctypes.c_uint32),
+    ]
+
+
+class PkError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load the HIP library; raise loudly if it is absent (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise PkError(f"{path} not found: build it with `python -m pokegym_amd.build` "
+                      "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    L = ctypes.CDLL(path)
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    vp = ctypes.c_void_p
+    L.pk_create.argtypes = [ctypes.POINTER(PkConfig), ctypes.POINTER(vp)]
+    L.pk_destroy.argtypes = [vp]
+    L.pk_destroy.restype = None
+    L.pk_last_error.restype = ctypes.c_char_p
+    L.pk_reset.argtypes = [vp, vp, vp]
+    L.pk_step.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+    L.pk_screen_ptr.argtypes = [vp]
+    L.pk_screen_ptr.restype = vp
+    L.pk_num_envs.argtypes = [vp]
+    L.pk_num_envs.restype = ctypes.c_uint32
+    L.pk_peek.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint16, ctypes.c_uint32, u8p]
+    L.pk_poke.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint16, ctypes.c_uint32, u8p]
+    L.pk_snapshot.argtypes = [vp, ctypes.c_uint32, u8p, ctypes.c_uint64]
+    L.pk_load_env.argtypes = [vp, ctypes.c_uint32, u8p, ctypes.c_uint64]
+    L.pk_last_instr_count.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().pk_last_error().decode(errors="replace")
+        raise PkError(f"{what} failed ({rc}): {msg}")

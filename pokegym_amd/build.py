@@ -1,0 +1,55 @@
+"""Build the HIP extension (gfx950) in-tree: pokegym_amd/lib/libpokegym_amd.so.
+
+hipcc cross-compiles for gfx950 without a GPU, so this runs in the build container and the
+resulting .so travels to the GPU box with the repository snapshot.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+LIB = os.path.join(LIBDIR, "libpokegym_amd.so")
+SOURCES = ["pk_kernels.hip", "pk_capi.cpp"]
+HEADERS = ["pk_layout.h", "pk_decode.h", os.path.join("..", "..", "include", "pokegym_amd.h")]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("PK_OFFLOAD_ARCH", "gfx950")
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.abspath(__file__)]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    os.makedirs(LIBDIR, exist_ok=True)
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + ".o")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+               "-Wno-unused-function", "-c", "-o", obj]
+        if src.endswith(".cpp"):
+            cmd += ["-x", "hip"]
+        cmd.append(os.path.join(CSRC, src))
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    tmp = LIB + ".tmp"
+    subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs, check=True)
+    os.replace(tmp, LIB)
+    for o in objs:
+        os.remove(o)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,518 @@
+// pk_capi.cpp — the C ABI (include/pokegym_amd.h) over the HIP kernels in pk_kernels.hip.
+//
+// Owns the per-GPU device state: lane-interleaved RAM images, SoA lane registers, per-line
+// render latches, the persistent grey screen, the ROM and the decode table, plus a parsed copy
+// of the template savestate used by pk_reset.  Savestate import/export restates the PyBoy v9
+// layout pinned on the reference's 264 savestates (oracle/gbcore.c load/save).
+#include <hip/hip_runtime.h>
+
+#include <errno.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/pokegym_amd.h"
+#include "pk_decode.h"
+#include "pk_layout.h"
+
+hipError_t pk_launch_step(const PkStepArgs& a, hipStream_t s);
+hipError_t pk_launch_render(const PkStepArgs& a, hipStream_t s);
+hipError_t pk_launch_reset(const PkResetArgs& a, hipStream_t s);
+hipError_t pk_launch_gather_env(const uint8_t* mem, uint32_t env, uint8_t* out, hipStream_t s);
+hipError_t pk_launch_scatter_env(uint8_t* mem, uint32_t env, const uint8_t* in, hipStream_t s);
+hipError_t pk_launch_done(const uint32_t* time_reg, uint32_t n, uint32_t max_steps, uint8_t* term,
+                          uint8_t* trunc, double* rew, hipStream_t s);
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                       \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess) return fail(-EIO, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+// v9 savestate offsets
+constexpr size_t S_VER = 0, S_HDR = 1, S_CPU = 5, S_VRAM = 23, S_OAM = 8215, S_LCDREG = 8375,
+                 S_LCDX = 8386, S_CLOCK = 8388, S_TARGET = 8396, S_NEXTMODE = 8404,
+                 S_SCAN = 8405, S_SCREEN = 9125, S_WRAM = 101285, S_FEA0 = 109477,
+                 S_IO = 109573, S_HRAM = 109649, S_FF4C = 109776, S_TIMER = 109828,
+                 S_MBC = 109836, S_SRAM = 109842, S_SIZE = 142610;
+
+struct Template {
+    uint32_t regs[PK_NREGS];
+    std::vector<uint8_t> mem;       // PK_PHYS
+    uint32_t lat[3 * PK_ROWS];
+    std::vector<uint8_t> screen;    // 144*160 grey
+    uint8_t hdr[4];
+    uint8_t lcdx[2];
+};
+
+uint64_t rd64(const uint8_t* p) {
+    uint64_t v = 0;
+    for (int i = 7; i >= 0; i--) v = (v << 8) | p[i];
+    return v;
+}
+void wr64(uint8_t* p, uint64_t v) {
+    for (int i = 0; i < 8; i++) { p[i] = (uint8_t)v; v >>= 8; }
+}
+
+int parse_v9(const uint8_t* s, size_t len, Template& t) {
+    if (len != S_SIZE || s[S_VER] != 9) return fail(-EINVAL, "not a PyBoy v9 savestate (len %zu)", len);
+    uint64_t clock = rd64(s + S_CLOCK), target = rd64(s + S_TARGET);
+    if (clock > 0xFFFFFFFFull || target > 0xFFFFFFFFull) return fail(-EINVAL, "LCD clock out of range");
+    memset(t.regs, 0, sizeof t.regs);
+    const uint8_t* c = s + S_CPU;  // A F B C D E HL SP PC ime halted stopped IE queued IF
+    t.regs[PK_R_W0] = c[3] | (c[2] << 8) | (c[5] << 16) | ((uint32_t)c[4] << 24);
+    t.regs[PK_R_W1] = c[6] | (c[7] << 8) | (c[0] << 16) | ((uint32_t)c[1] << 24);
+    t.regs[PK_R_SP] = c[8] | (c[9] << 8);
+    t.regs[PK_R_PC] = c[10] | (c[11] << 8);
+    t.regs[PK_R_CPU] = (c[12] ? 1u : 0u) | (c[13] ? 2u : 0u) | (c[16] ? 4u : 0u) | (c[14] ? 16u : 0u) |
+                       ((uint32_t)c[15] << 8) | ((uint32_t)c[17] << 16);
+    t.regs[PK_R_CLOCK] = (uint32_t)clock;
+    t.regs[PK_R_TARGET] = (uint32_t)target;
+    const uint8_t* r = s + S_LCDREG;  // LCDC BGP OBP0 OBP1 STAT LY LYC SCY SCX WY WX
+    t.regs[PK_R_LCD0] = r[0] | (r[4] << 8) | (r[5] << 16) | ((uint32_t)r[6] << 24);
+    t.regs[PK_R_LCD1] = r[7] | (r[8] << 8) | (r[9] << 16) | ((uint32_t)r[10] << 24);
+    t.regs[PK_R_LCD2] = r[1] | (r[2] << 8) | (r[3] << 16) | ((uint32_t)s[S_NEXTMODE] << 24);
+    const uint8_t* tm = s + S_TIMER;  // DIV TIMA DIVc(le16) TIMAc(le16) TMA TAC
+    t.regs[PK_R_TIM0] = tm[0] | (tm[1] << 8) | (tm[6] << 16) | ((uint32_t)tm[7] << 24);
+    t.regs[PK_R_TIM1] = (tm[2] | (tm[3] << 8)) | ((uint32_t)(tm[4] | (tm[5] << 8)) << 16);
+    const uint8_t* mb = s + S_MBC;
+    t.regs[PK_R_MBC] = mb[0] | (mb[1] << 8) | (mb[2] << 16) | ((uint32_t)mb[3] << 24);
+    t.regs[PK_R_MISC] = 0x0Fu | (0x0Fu << 8);  // no button held, ly_window = -1
+    t.mem.assign(PK_PHYS, 0);
+    memcpy(&t.mem[PK_P_VRAM], s + S_VRAM, 8192);
+    memcpy(&t.mem[PK_P_WRAM], s + S_WRAM, 8192);
+    memcpy(&t.mem[PK_P_OAM], s + S_OAM, 160);
+    memcpy(&t.mem[PK_P_OAM + 0xA0], s + S_FEA0, 96);
+    memcpy(&t.mem[PK_P_IO], s + S_IO, 76);
+    memcpy(&t.mem[PK_P_IO + 0x4C], s + S_FF4C, 52);
+    memcpy(&t.mem[PK_P_HRAM], s + S_HRAM, 127);
+    memcpy(&t.mem[PK_P_SRAM], s + S_SRAM, 4 * 8192);
+    t.screen.resize(PK_SCREEN);
+    for (size_t i = 0; i < PK_SCREEN; i++) t.screen[i] = s[S_SCREEN + i * 4 + 1];
+    for (uint32_t y = 0; y < PK_ROWS; y++) {
+        const uint8_t* p = s + S_SCAN + y * 5;  // SCX SCY WX WY tiledata_select
+        uint32_t lcdc = (r[0] & ~0x10u) | ((p[4] & 1u) << 4);
+        t.lat[y] = lcdc | (p[0] << 8) | (p[1] << 16) | ((uint32_t)p[2] << 24);
+        t.lat[PK_ROWS + y] = p[3] | (r[1] << 8) | (r[2] << 16) | ((uint32_t)r[3] << 24);
+        t.lat[2 * PK_ROWS + y] = 0;
+    }
+    memcpy(t.hdr, s + S_HDR, 4);
+    t.lcdx[0] = s[S_LCDX];
+    t.lcdx[1] = s[S_LCDX + 1];
+    return 0;
+}
+
+void power_on(Template& t) {
+    // our own post-boot DMG state (PyBoy would execute its bundled boot ROM instead);
+    // identical to oracle/gbcore.c gb_power_on
+    memset(t.regs, 0, sizeof t.regs);
+    t.regs[PK_R_W0] = 0x13 | (0x00 << 8) | (0xD8 << 16) | (0x00u << 24);
+    t.regs[PK_R_W1] = 0x4D | (0x01 << 8) | (0x01 << 16) | (0xB0u << 24);
+    t.regs[PK_R_SP] = 0xFFFE;
+    t.regs[PK_R_PC] = 0x0100;
+    t.regs[PK_R_CPU] = 0;
+    t.regs[PK_R_CLOCK] = 0;
+    t.regs[PK_R_TARGET] = 80;
+    t.regs[PK_R_LCD0] = 0x91 | (0x82 << 8);
+    t.regs[PK_R_LCD1] = 0;
+    t.regs[PK_R_LCD2] = 0xFC | (0xFF << 8) | (0xFF << 16) | (3u << 24);
+    t.regs[PK_R_TIM0] = 0xAB;
+    t.regs[PK_R_TIM1] = 0;
+    t.regs[PK_R_MBC] = 1;
+    t.regs[PK_R_MISC] = 0x0Fu | (0x0Fu << 8);
+    t.mem.assign(PK_PHYS, 0);
+    t.mem[PK_P_IO] = 0xCF;
+    t.screen.assign(PK_SCREEN, 0xFF);  // shade 0
+    for (uint32_t y = 0; y < PK_ROWS; y++) {
+        t.lat[y] = 0;
+        t.lat[PK_ROWS + y] = 0;
+        t.lat[2 * PK_ROWS + y] = 0;
+    }
+    memset(t.hdr, 0, 4);
+    t.lcdx[0] = t.lcdx[1] = 0;
+}
+
+uint8_t grey_to_flag(uint8_t g) { return g == 0xFF ? 1 : 0; }
+
+void export_v9(const Template& tp, const uint32_t* regs, const uint8_t* mem, const uint32_t* lat,
+               const uint8_t* screen, uint8_t* s) {
+    memset(s, 0, S_SIZE);
+    s[S_VER] = 9;
+    memcpy(s + S_HDR, tp.hdr, 4);
+    uint32_t w0 = regs[PK_R_W0], w1 = regs[PK_R_W1];
+    uint8_t* c = s + S_CPU;
+    c[0] = (w1 >> 16) & 0xFF; c[1] = (w1 >> 24) & 0xFF;  // A F
+    c[2] = (w0 >> 8) & 0xFF; c[3] = w0 & 0xFF;            // B C
+    c[4] = (w0 >> 24) & 0xFF; c[5] = (w0 >> 16) & 0xFF;   // D E
+    c[6] = w1 & 0xFF; c[7] = (w1 >> 8) & 0xFF;            // HL
+    c[8] = regs[PK_R_SP] & 0xFF; c[9] = (regs[PK_R_SP] >> 8) & 0xFF;
+    c[10] = regs[PK_R_PC] & 0xFF; c[11] = (regs[PK_R_PC] >> 8) & 0xFF;
+    uint32_t cpu = regs[PK_R_CPU];
+    c[12] = cpu & 1; c[13] = (cpu >> 1) & 1; c[14] = (cpu >> 4) & 1;
+    c[15] = (cpu >> 8) & 0xFF; c[16] = (cpu >> 2) & 1; c[17] = (cpu >> 16) & 0xFF;
+    memcpy(s + S_VRAM, mem + PK_P_VRAM, 8192);
+    memcpy(s + S_OAM, mem + PK_P_OAM, 160);
+    uint32_t l0 = regs[PK_R_LCD0], l1 = regs[PK_R_LCD1], l2 = regs[PK_R_LCD2];
+    uint8_t* r = s + S_LCDREG;
+    r[0] = l0 & 0xFF; r[1] = l2 & 0xFF; r[2] = (l2 >> 8) & 0xFF; r[3] = (l2 >> 16) & 0xFF;
+    r[4] = (l0 >> 8) & 0xFF; r[5] = (l0 >> 16) & 0xFF; r[6] = (l0 >> 24) & 0xFF;
+    r[7] = l1 & 0xFF; r[8] = (l1 >> 8) & 0xFF; r[9] = (l1 >> 16) & 0xFF; r[10] = (l1 >> 24) & 0xFF;
+    s[S_LCDX] = tp.lcdx[0];
+    s[S_LCDX + 1] = tp.lcdx[1];
+    wr64(s + S_CLOCK, regs[PK_R_CLOCK]);
+    wr64(s + S_TARGET, regs[PK_R_TARGET]);
+    s[S_NEXTMODE] = (l2 >> 24) & 0xFF;
+    for (uint32_t y = 0; y < PK_ROWS; y++) {
+        uint32_t a = lat[y], b = lat[PK_ROWS + y];
+        uint8_t* p = s + S_SCAN + y * 5;
+        p[0] = (a >> 8) & 0xFF; p[1] = (a >> 16) & 0xFF; p[2] = (a >> 24) & 0xFF; p[3] = b & 0xFF;
+        p[4] = (a >> 4) & 1;
+    }
+    for (size_t i = 0; i < PK_SCREEN; i++) {
+        uint8_t g = screen[i];
+        s[S_SCREEN + i * 4 + 0] = grey_to_flag(g);
+        s[S_SCREEN + i * 4 + 1] = s[S_SCREEN + i * 4 + 2] = s[S_SCREEN + i * 4 + 3] = g;
+    }
+    memcpy(s + S_WRAM, mem + PK_P_WRAM, 8192);
+    memcpy(s + S_FEA0, mem + PK_P_OAM + 0xA0, 96);
+    memcpy(s + S_IO, mem + PK_P_IO, 76);
+    memcpy(s + S_HRAM, mem + PK_P_HRAM, 127);
+    memcpy(s + S_FF4C, mem + PK_P_IO + 0x4C, 52);
+    uint32_t t0 = regs[PK_R_TIM0], t1 = regs[PK_R_TIM1];
+    uint8_t* tm = s + S_TIMER;
+    tm[0] = t0 & 0xFF; tm[1] = (t0 >> 8) & 0xFF;
+    tm[2] = t1 & 0xFF; tm[3] = (t1 >> 8) & 0xFF; tm[4] = (t1 >> 16) & 0xFF; tm[5] = (t1 >> 24) & 0xFF;
+    tm[6] = (t0 >> 16) & 0xFF; tm[7] = (t0 >> 24) & 0xFF;
+    uint32_t mbc = regs[PK_R_MBC];
+    uint8_t* m = s + S_MBC;
+    m[0] = mbc & 0xFF; m[1] = (mbc >> 8) & 0xFF; m[2] = (mbc >> 16) & 0xFF; m[3] = (mbc >> 24) & 0xFF;
+    memcpy(s + S_SRAM, mem + PK_P_SRAM, 4 * 8192);
+}
+
+}  // namespace
+
+struct pk_handle {
+    int device = 0;
+    uint32_t n = 0, npad = 0, ngroups = 0;
+    uint32_t frames = 24, release = 8, flags = 0, max_steps = 20480;
+    uint32_t mbc = 3, bank_mask = 0;
+    uint8_t* mem = nullptr;
+    uint32_t* regs = nullptr;
+    uint32_t* lat = nullptr;
+    uint8_t* screen = nullptr;
+    uint8_t* rom = nullptr;
+    uint32_t* dtab = nullptr;
+    uint8_t* t_mem = nullptr;
+    uint32_t* t_regs = nullptr;
+    uint32_t* t_lat = nullptr;
+    uint8_t* t_screen = nullptr;
+    uint8_t* scratch = nullptr;  // PK_PHYS staging for one env
+    size_t lat_stride = 0;
+    Template tmpl;
+};
+
+extern "C" {
+
+const char* pk_last_error(void) { return g_err.c_str(); }
+int pk_abi_version(void) { return PK_ABI_VERSION; }
+uint8_t* pk_screen_ptr(pk_handle* h) { return h ? h->screen : nullptr; }
+uint32_t pk_num_envs(const pk_handle* h) { return h ? h->n : 0; }
+
+void pk_destroy(pk_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    void* ptrs[] = {h->mem, h->regs, h->lat, h->screen, h->rom, h->dtab, h->t_mem, h->t_regs,
+                    h->t_lat, h->t_screen, h->scratch};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    delete h;
+}
+
+int pk_create(const pk_config* cfg, pk_handle** out) {
+    if (!cfg || !out) return fail(-EINVAL, "null argument");
+    *out = nullptr;
+    if (cfg->n_envs == 0) return fail(-EINVAL, "n_envs must be > 0");
+    if (!cfg->rom || cfg->rom_len < 0x8000 || (cfg->rom_len & 0x3FFF))
+        return fail(-EINVAL, "ROM must be a multiple of 16 KiB and >= 32 KiB");
+    uint32_t banks = (uint32_t)(cfg->rom_len / 0x4000);
+    if (banks & (banks - 1)) return fail(-EINVAL, "ROM bank count must be a power of two");
+    uint8_t type = cfg->rom[0x147];
+    uint32_t mbc;
+    if (type == 0x00) mbc = 0;
+    else if (type >= 0x0F && type <= 0x13) mbc = 3;
+    else return fail(-ENOTSUP, "cartridge type 0x%02x not supported (ROM-only and MBC3 are)", type);
+    if (cfg->frame_skip == 0 || cfg->frame_skip > 1024) return fail(-EINVAL, "bad frame_skip");
+
+    pk_handle* h = new pk_handle();
+    h->device = cfg->device;
+    h->n = cfg->n_envs;
+    h->npad = (cfg->n_envs + PK_LANES - 1) / PK_LANES * PK_LANES;
+    h->ngroups = h->npad / PK_LANES;
+    h->frames = cfg->frame_skip;
+    h->release = cfg->release_frame;
+    h->flags = cfg->flags;
+    h->max_steps = cfg->max_episode_steps ? cfg->max_episode_steps : 20480;
+    h->mbc = mbc;
+    h->bank_mask = banks - 1;
+    h->lat_stride = (size_t)h->ngroups * PK_ROWS * PK_LANES;
+    int rc;
+    if (cfg->state) {
+        if ((rc = parse_v9(cfg->state, cfg->state_len, h->tmpl))) { delete h; return rc; }
+    } else {
+        power_on(h->tmpl);
+    }
+#define ALLOC(ptr, bytes)                                                                  \
+    do {                                                                                   \
+        hipError_t e_ = hipMalloc((void**)&(ptr), (bytes));                                \
+        if (e_ != hipSuccess) {                                                            \
+            pk_destroy(h);                                                                 \
+            return fail(-ENOMEM, "hipMalloc(%zu): %s", (size_t)(bytes), hipGetErrorString(e_)); \
+        }                                                                                  \
+    } while (0)
+    if (hipSetDevice(h->device) != hipSuccess) { delete h; return fail(-ENODEV, "hipSetDevice(%d) failed", cfg->device); }
+    ALLOC(h->mem, (size_t)h->ngroups * PK_GROUP_STRIDE);
+    ALLOC(h->regs, (size_t)PK_NREGS * h->npad * 4);
+    ALLOC(h->lat, 3 * h->lat_stride * 4);
+    ALLOC(h->screen, (size_t)h->npad * PK_SCREEN);
+    ALLOC(h->rom, cfg->rom_len);
+    ALLOC(h->dtab, 512 * 4);
+    ALLOC(h->t_mem, PK_PHYS);
+    ALLOC(h->t_regs, PK_NREGS * 4);
+    ALLOC(h->t_lat, 3 * PK_ROWS * 4);
+    ALLOC(h->t_screen, PK_SCREEN);
+    ALLOC(h->scratch, PK_PHYS + PK_NREGS * 4 + 3 * PK_ROWS * 4 + PK_SCREEN);
+#undef ALLOC
+    uint32_t dt[512];
+    pk_build_decode(dt);
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = hipMemcpy(h->rom, cfg->rom, cfg->rom_len, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->dtab, dt, sizeof dt, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->t_mem, h->tmpl.mem.data(), PK_PHYS, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->t_regs, h->tmpl.regs, sizeof h->tmpl.regs, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->t_lat, h->tmpl.lat, sizeof h->tmpl.lat, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->t_screen, h->tmpl.screen.data(), PK_SCREEN, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(h->regs, 0, (size_t)PK_NREGS * h->npad * 4);
+    if (e == hipSuccess) e = hipMemset(h->lat, 0, 3 * h->lat_stride * 4);
+    if (e != hipSuccess) {
+        pk_destroy(h);
+        return fail(-EIO, "device upload failed: %s", hipGetErrorString(e));
+    }
+    if ((rc = pk_reset(h, nullptr, nullptr))) { pk_destroy(h); return rc; }
+    if (hipDeviceSynchronize() != hipSuccess) { pk_destroy(h); return fail(-EIO, "initial reset failed"); }
+    *out = h;
+    return 0;
+}
+
+int pk_reset(pk_handle* h, const uint8_t* mask, void* stream) {
+    if (!h) return fail(-EINVAL, "null handle");
+    HIPCHK(hipSetDevice(h->device));
+    PkResetArgs a;
+    a.mem = h->mem; a.regs = h->regs; a.lat = h->lat; a.screen = h->screen;
+    a.tmpl_mem = h->t_mem; a.tmpl_regs = h->t_regs; a.tmpl_lat = h->t_lat; a.tmpl_screen = h->t_screen;
+    a.mask = mask; a.n = h->n; a.npad = h->npad; a.lat_stride = (uint32_t)h->lat_stride;
+    HIPCHK(pk_launch_reset(a, (hipStream_t)stream));
+    return 0;
+}
+
+int pk_step(pk_handle* h, const uint8_t* actions, uint8_t* screen_out, double* rew, uint8_t* term,
+            uint8_t* trunc, void* stream) {
+    if (!h) return fail(-EINVAL, "null handle");
+    if (!actions) return fail(-EINVAL, "actions_dev is required");
+    HIPCHK(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    PkStepArgs a;
+    a.mem = h->mem; a.rom = h->rom; a.regs = h->regs; a.dtab = h->dtab; a.actions = actions;
+    a.lat = h->lat; a.screen = h->screen; a.n = h->n; a.npad = h->npad;
+    a.rom_bank_mask = h->bank_mask; a.mbc = h->mbc; a.frames = h->frames;
+    a.release_frame = h->release; a.render_last = (h->flags & PK_F_RENDER) ? 1 : 0;
+    a.lat_stride = (uint32_t)h->lat_stride;
+    HIPCHK(pk_launch_step(a, s));
+    if (a.render_last) HIPCHK(pk_launch_render(a, s));
+    if (screen_out)
+        HIPCHK(hipMemcpyAsync(screen_out, h->screen, (size_t)h->n * PK_SCREEN, hipMemcpyDeviceToDevice, s));
+    if (rew || term || trunc)
+        HIPCHK(pk_launch_done(h->regs + (size_t)PK_R_TIME * h->npad, h->n, h->max_steps, term, trunc, rew, s));
+    return 0;
+}
+
+// gather one env's full state to host: mem (PK_PHYS), regs, latches, screen
+static int fetch_env(pk_handle* h, uint32_t env, std::vector<uint8_t>& mem, uint32_t* regs,
+                     uint32_t* lat, std::vector<uint8_t>& screen) {
+    if (env >= h->n) return fail(-EINVAL, "env %u out of range (n=%u)", env, h->n);
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(pk_launch_gather_env(h->mem, env, h->scratch, nullptr));
+    mem.resize(PK_PHYS);
+    HIPCHK(hipMemcpy(mem.data(), h->scratch, PK_PHYS, hipMemcpyDeviceToHost));
+    for (uint32_t f = 0; f < PK_NREGS; f++)
+        HIPCHK(hipMemcpy(&regs[f], h->regs + (size_t)f * h->npad + env, 4, hipMemcpyDeviceToHost));
+    uint32_t gid = env / PK_LANES, lane = env % PK_LANES;
+    for (uint32_t k = 0; k < 3; k++) {
+        std::vector<uint32_t> tmp((size_t)PK_ROWS * PK_LANES);
+        HIPCHK(hipMemcpy(tmp.data(), h->lat + k * h->lat_stride + (size_t)gid * PK_ROWS * PK_LANES,
+                         tmp.size() * 4, hipMemcpyDeviceToHost));
+        for (uint32_t y = 0; y < PK_ROWS; y++) lat[k * PK_ROWS + y] = tmp[(size_t)y * PK_LANES + lane];
+    }
+    screen.resize(PK_SCREEN);
+    HIPCHK(hipMemcpy(screen.data(), h->screen + (size_t)env * PK_SCREEN, PK_SCREEN, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int pk_snapshot(pk_handle* h, uint32_t env, uint8_t* out, uint64_t len) {
+    if (!h || !out) return fail(-EINVAL, "null argument");
+    if (len < S_SIZE) return fail(-EINVAL, "buffer too small for a v9 state");
+    std::vector<uint8_t> mem, screen;
+    uint32_t regs[PK_NREGS], lat[3 * PK_ROWS];
+    int rc = fetch_env(h, env, mem, regs, lat, screen);
+    if (rc) return rc;
+    export_v9(h->tmpl, regs, mem.data(), lat, screen.data(), out);
+    return 0;
+}
+
+int pk_load_env(pk_handle* h, uint32_t env, const uint8_t* in, uint64_t len) {
+    if (!h || !in) return fail(-EINVAL, "null argument");
+    if (env >= h->n) return fail(-EINVAL, "env %u out of range", env);
+    Template t;
+    int rc = parse_v9(in, len, t);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(h->scratch, t.mem.data(), PK_PHYS, hipMemcpyHostToDevice));
+    HIPCHK(pk_launch_scatter_env(h->mem, env, h->scratch, nullptr));
+    HIPCHK(hipDeviceSynchronize());
+    for (uint32_t f = 0; f < PK_NREGS; f++)
+        HIPCHK(hipMemcpy(h->regs + (size_t)f * h->npad + env, &t.regs[f], 4, hipMemcpyHostToDevice));
+    uint32_t gid = env / PK_LANES, lane = env % PK_LANES;
+    for (uint32_t k = 0; k < 3; k++)
+        for (uint32_t y = 0; y < PK_ROWS; y++)
+            HIPCHK(hipMemcpy(h->lat + k * h->lat_stride + ((size_t)gid * PK_ROWS + y) * PK_LANES + lane,
+                             &t.lat[k * PK_ROWS + y], 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->screen + (size_t)env * PK_SCREEN, t.screen.data(), PK_SCREEN, hipMemcpyHostToDevice));
+    return 0;
+}
+
+// guest-address view of one env's memory (PyBoy get_memory_value semantics for RAM regions and
+// the special IO registers)
+static int guest_phys(uint32_t addr, const uint32_t* regs, uint32_t mbc, uint32_t* phys, int* special) {
+    *special = -1;
+    if (addr < 0x8000) return -1;
+    if (addr < 0xA000) { *phys = PK_P_VRAM + addr - 0x8000; return 0; }
+    if (addr < 0xC000) {
+        uint32_t m = regs[PK_R_MBC];
+        if (mbc == 0 || !((m >> 16) & 0xFF)) return -2;
+        *phys = PK_P_SRAM + (((m >> 8) & 3) * 0x2000) + (addr - 0xA000);
+        return 0;
+    }
+    if (addr < 0xFE00) { *phys = PK_P_WRAM + (addr & 0x1FFF); return 0; }
+    if (addr < 0xFF00) { *phys = PK_P_OAM + (addr - 0xFE00); return 0; }
+    if (addr >= 0xFF80) {
+        if (addr == 0xFFFF) { *special = (int)addr; return 1; }
+        *phys = PK_P_HRAM + addr - 0xFF80;
+        return 0;
+    }
+    if ((addr >= 0xFF04 && addr <= 0xFF07) || addr == 0xFF0F || (addr >= 0xFF10 && addr <= 0xFF4B)) {
+        *special = (int)addr;
+        return 1;
+    }
+    *phys = PK_P_IO + (addr - 0xFF00);
+    return 0;
+}
+
+static uint8_t special_read(uint32_t a, const uint32_t* R) {
+    auto b = [](uint32_t v, int sh) { return (uint8_t)((v >> sh) & 0xFF); };
+    switch (a) {
+        case 0xFF04: return b(R[PK_R_TIM0], 0);
+        case 0xFF05: return b(R[PK_R_TIM0], 8);
+        case 0xFF06: return b(R[PK_R_TIM0], 16);
+        case 0xFF07: return b(R[PK_R_TIM0], 24);
+        case 0xFF0F: return b(R[PK_R_CPU], 16);
+        case 0xFF40: return b(R[PK_R_LCD0], 0);
+        case 0xFF41: return b(R[PK_R_LCD0], 8);
+        case 0xFF42: return b(R[PK_R_LCD1], 0);
+        case 0xFF43: return b(R[PK_R_LCD1], 8);
+        case 0xFF44: return b(R[PK_R_LCD0], 16);
+        case 0xFF45: return b(R[PK_R_LCD0], 24);
+        case 0xFF47: return b(R[PK_R_LCD2], 0);
+        case 0xFF48: return b(R[PK_R_LCD2], 8);
+        case 0xFF49: return b(R[PK_R_LCD2], 16);
+        case 0xFF4A: return b(R[PK_R_LCD1], 16);
+        case 0xFF4B: return b(R[PK_R_LCD1], 24);
+        case 0xFFFF: return b(R[PK_R_CPU], 8);
+        default: return 0;
+    }
+}
+
+int pk_peek(pk_handle* h, uint32_t env, uint16_t addr, uint32_t len, uint8_t* out) {
+    if (!h || !out) return fail(-EINVAL, "null argument");
+    if ((uint32_t)addr + len > 0x10000u) return fail(-EINVAL, "range past 0xFFFF");
+    std::vector<uint8_t> mem, screen;
+    uint32_t regs[PK_NREGS], lat[3 * PK_ROWS];
+    int rc = fetch_env(h, env, mem, regs, lat, screen);
+    if (rc) return rc;
+    std::vector<uint8_t> rom;
+    for (uint32_t i = 0; i < len; i++) {
+        uint32_t a = (uint32_t)addr + i, phys;
+        int special;
+        int k = guest_phys(a, regs, h->mbc, &phys, &special);
+        if (k == 0) out[i] = mem[phys];
+        else if (k == 1) out[i] = special_read(a, regs);
+        else if (k == -2) out[i] = 0xFF;
+        else {
+            // ROM read
+            uint32_t off = a < 0x4000 ? a : ((regs[PK_R_MBC] & 0xFF) & h->bank_mask) * 0x4000u + (a - 0x4000u);
+            HIPCHK(hipMemcpy(&out[i], h->rom + off, 1, hipMemcpyDeviceToHost));
+        }
+    }
+    return 0;
+}
+
+int pk_poke(pk_handle* h, uint32_t env, uint16_t addr, uint32_t len, const uint8_t* in) {
+    if (!h || !in) return fail(-EINVAL, "null argument");
+    if (env >= h->n) return fail(-EINVAL, "env %u out of range", env);
+    if ((uint32_t)addr + len > 0x10000u) return fail(-EINVAL, "range past 0xFFFF");
+    std::vector<uint8_t> mem, screen;
+    uint32_t regs[PK_NREGS], lat[3 * PK_ROWS];
+    int rc = fetch_env(h, env, mem, regs, lat, screen);
+    if (rc) return rc;
+    uint32_t gid = env / PK_LANES, lane = env % PK_LANES;
+    for (uint32_t i = 0; i < len; i++) {
+        uint32_t a = (uint32_t)addr + i, phys;
+        int special;
+        if (guest_phys(a, regs, h->mbc, &phys, &special) != 0)
+            return fail(-ENOTSUP, "pk_poke supports RAM regions only (addr 0x%04x)", a);
+        HIPCHK(hipMemcpy(h->mem + (size_t)gid * PK_GROUP_STRIDE + (size_t)phys * PK_LANES + lane, &in[i], 1,
+                         hipMemcpyHostToDevice));
+    }
+    return 0;
+}
+
+int pk_last_instr_count(pk_handle* h, uint64_t* out) {
+    if (!h || !out) return fail(-EINVAL, "null argument");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    std::vector<uint32_t> v(h->n);
+    HIPCHK(hipMemcpy(v.data(), h->regs + (size_t)PK_R_ICOUNT * h->npad, (size_t)h->n * 4, hipMemcpyDeviceToHost));
+    uint64_t s = 0;
+    for (uint32_t x : v) s += x;
+    *out = s;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,123 @@
+"""BatchedEmulator — N Game Boys on one MI355X behind the C ABI (include/pokegym_amd.h).
+
+This is the device-side replacement of pokegym's per-process PyBoy instance
+(pokegym/pyboy_binding.py:42-91): one call to `step(actions)` advances every env by one
+env-step (press, 24 frames, release before frame 8, rasterise frame 24) inside one HIP launch.
+Device buffers are PyTorch-ROCm tensors; the kernels run on the caller's current HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native
+from ._native import PK_F_RENDER, STATE_V9_BYTES, ROWS, COLS, check
+
+
+class _CudaArray:
+    """__cuda_array_interface__ shim to wrap a handle-owned device buffer without a copy."""
+
+    def __init__(self, ptr: int, shape, typestr: str):
+        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": typestr,
+                                         "data": (ptr, False), "version": 2, "strides": None}
+
+
+def _u8p(buf: bytes | bytearray | np.ndarray):
+    a = np.frombuffer(bytes(buf), dtype=np.uint8) if not isinstance(buf, np.ndarray) else buf
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    return a, a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+class BatchedEmulator:
+    def __init__(self, rom: bytes, n_envs: int, state: bytes | None = None, device: int = 0,
+                 frame_skip: int = 24, release_frame: int = 8, render: bool = True,
+                 max_episode_steps: int = 20480):
+        self._L = _native.load()
+        if not torch.cuda.is_available():
+            raise _native.PkError("no ROCm GPU visible: the HIP path has no CPU fallback")
+        self.device = torch.device("cuda", device)
+        self.n = int(n_envs)
+        self._rom, rom_p = _u8p(rom)
+        cfg = _native.PkConfig()
+        cfg.n_envs = self.n
+        cfg.device = device
+        cfg.rom = rom_p
+        cfg.rom_len = len(self._rom)
+        if state is not None:
+            self._state, st_p = _u8p(state)
+            cfg.state = st_p
+            cfg.state_len = len(self._state)
+        cfg.frame_skip = frame_skip
+        cfg.release_frame = release_frame
+        cfg.flags = PK_F_RENDER if render else 0
+        cfg.max_episode_steps = max_episode_steps
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(self._L.pk_create(ctypes.byref(cfg), ctypes.byref(h)), "pk_create")
+        self._h = h
+        self.render = render
+        ptr = self._L.pk_screen_ptr(self._h)
+        self.screen = torch.as_tensor(_CudaArray(ptr, (self.n, ROWS, COLS), "|u1"), device=self.device)
+        self.rewards = torch.zeros(self.n, dtype=torch.float64, device=self.device)
+        self.terminals = torch.zeros(self.n, dtype=torch.uint8, device=self.device)
+        self.truncations = torch.zeros(self.n, dtype=torch.uint8, device=self.device)
+
+    # -- stream helpers -----------------------------------------------------------------
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # -- hot path -----------------------------------------------------------------------
+    def step(self, actions: torch.Tensor):
+        """actions: uint8[n] on this device. Returns (screen, rewards, terminals, truncations)."""
+        if actions.dtype != torch.uint8 or actions.device != self.device or actions.numel() != self.n:
+            raise ValueError("actions must be a uint8 tensor of n_envs elements on the emulator's device")
+        actions = actions.contiguous()
+        check(self._L.pk_step(self._h, ctypes.c_void_p(actions.data_ptr()), None,
+                              ctypes.c_void_p(self.rewards.data_ptr()),
+                              ctypes.c_void_p(self.terminals.data_ptr()),
+                              ctypes.c_void_p(self.truncations.data_ptr()), self._stream()), "pk_step")
+        return self.screen, self.rewards, self.terminals, self.truncations
+
+    def reset(self, mask: torch.Tensor | None = None):
+        mp = None if mask is None else ctypes.c_void_p(mask.to(torch.uint8).contiguous().data_ptr())
+        check(self._L.pk_reset(self._h, mp, self._stream()), "pk_reset")
+
+    # -- host-side accessors (synchronous) --------------------------------------------
+    def snapshot(self, env: int) -> bytes:
+        out = np.zeros(STATE_V9_BYTES, np.uint8)
+        check(self._L.pk_snapshot(self._h, env, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), len(out)),
+              "pk_snapshot")
+        return out.tobytes()
+
+    def load_env(self, env: int, state: bytes):
+        a, p = _u8p(state)
+        check(self._L.pk_load_env(self._h, env, p, len(a)), "pk_load_env")
+
+    def peek(self, env: int, addr: int, n: int = 1) -> bytes:
+        out = np.zeros(n, np.uint8)
+        check(self._L.pk_peek(self._h, env, addr, n, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))), "pk_peek")
+        return out.tobytes()
+
+    def poke(self, env: int, addr: int, data: bytes):
+        a, p = _u8p(data)
+        check(self._L.pk_poke(self._h, env, addr, len(a), p), "pk_poke")
+
+    def last_instr_count(self) -> int:
+        v = ctypes.c_uint64()
+        check(self._L.pk_last_instr_count(self._h, ctypes.byref(v)), "pk_last_instr_count")
+        return int(v.value)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            torch.cuda.synchronize(self.device)
+            self.screen = None
+            self._L.pk_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass

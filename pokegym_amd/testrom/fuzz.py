@@ -1,0 +1,187 @@
+"""Seeded random SM83 programs for kernel-vs-oracle parity ("fuzz ROMs").
+
+Each ROM boots (post-boot state, PC=0x100), installs interrupt handlers for VBlank, STAT, timer
+and joypad, enables a random IE subset / TAC / STAT sources, copies an OAM-DMA stub to HRAM, and
+then loops forever over a few hundred random instruction blocks.  The blocks cover every legal
+opcode class: 8/16-bit loads (all addressing modes), ALU (reg, (HL), imm), INC/DEC, all CB ops,
+rotates, DAA/CPL/SCF/CCF, PUSH/POP, ADD SP,e / LD HL,SP+e / LD (nn),SP, JR/JP/CALL/RET/RST
+(conditional and not), RETI via the handlers, HALT, DI/EI, MBC3 ROM/SRAM bank switching, OAM DMA,
+LCD on/off, scroll/palette/window writes (visible in the rendered frame), joypad reads (so each
+env's action stream changes its control flow), DIV/TIMA/LY/STAT reads.
+"""
+from __future__ import annotations
+
+import random
+
+from .sm83asm import build_rom
+
+R8 = ["b", "c", "d", "e", "h", "l", "a"]
+ALU = ["add", "adc", "sub", "sbc", "and", "xor", "or", "cp"]
+CB = ["rlc", "rrc", "rl", "rr", "sla", "sra", "swap", "srl"]
+CC = ["nz", "z", "nc", "c"]
+IO_W = [0x42, 0x43, 0x47, 0x48, 0x49, 0x4A, 0x4B, 0x45, 0x41, 0x05, 0x06, 0x01, 0x02, 0x90]
+IO_R = [0x44, 0x41, 0x04, 0x05, 0x0F, 0x40, 0x42, 0x00, 0x47, 0x4A, 0xFF, 0x10, 0x26, 0x07]
+
+
+def _hl_anchor(rng: random.Random) -> str:
+    return f"ld hl, ${0xC000 + rng.randrange(0x0800, 0x1800):04x}"
+
+
+def _block(rng: random.Random, idx: int, n_banks: int, max_n: int = 14) -> list[str]:
+    out = []
+    for _ in range(rng.randint(min(4, max_n), max_n)):
+        k = rng.random()
+        r = rng.choice(R8)
+        if k < 0.10:
+            out.append(f"ld {r}, ${rng.randrange(256):02x}")
+        elif k < 0.17:
+            out.append(f"ld {rng.choice(R8)}, {rng.choice(R8)}")
+        elif k < 0.27:
+            op = rng.choice(ALU)
+            src = rng.choice(R8 + ["imm", "[hl]"])
+            if src == "imm":
+                out.append(f"{op} a, ${rng.randrange(256):02x}")
+            elif src == "[hl]":
+                out += [_hl_anchor(rng), f"{op} a, [hl]"]
+            else:
+                out.append(f"{op} a, {src}")
+        elif k < 0.32:
+            out.append(f"{rng.choice(['inc', 'dec'])} {rng.choice(R8)}")
+        elif k < 0.36:
+            out += [_hl_anchor(rng), f"{rng.choice(['inc', 'dec'])} [hl]"]
+        elif k < 0.42:
+            t = rng.choice(R8 + ["[hl]"])
+            pre = [_hl_anchor(rng)] if t == "[hl]" else []
+            g = rng.random()
+            if g < 0.4:
+                out += pre + [f"{rng.choice(CB)} {t}"]
+            else:
+                out += pre + [f"{rng.choice(['bit', 'res', 'set'])} {rng.randrange(8)}, {t}"]
+        elif k < 0.45:
+            out.append(rng.choice(["rlca", "rla", "rrca", "rra", "daa", "cpl", "scf", "ccf"]))
+        elif k < 0.48:
+            out += ["add a, $19" if rng.random() < 0.5 else "sub $27", "daa"]
+        elif k < 0.53:
+            out += [_hl_anchor(rng), rng.choice(["ld [hl+], a", "ld [hl-], a", "ld a, [hl+]", "ld a, [hl-]",
+                                               f"ld [hl], ${rng.randrange(256):02x}", f"ld [hl], {rng.choice(R8[:4] + ['a'])}",
+                                               f"ld {rng.choice(R8[:4] + ['a'])}, [hl]"])]
+        elif k < 0.56:
+            p = rng.choice(["bc", "de"])
+            out += [f"ld {p}, ${0xC000 + rng.randrange(0x800, 0x1800):04x}", f"ld [{p}], a" if rng.random() < 0.5 else f"ld a, [{p}]"]
+        elif k < 0.59:
+            a = 0xC000 + rng.randrange(0x800, 0x1800)
+            out.append(f"ld [${a:04x}], a" if rng.random() < 0.5 else f"ld a, [${a:04x}]")
+        elif k < 0.62:
+            p = rng.choice(["bc", "de", "hl"])
+            out.append(rng.choice([f"ld {p}, ${rng.randrange(65536):04x}", f"inc {p}", f"dec {p}", f"add hl, {p}"]))
+        elif k < 0.64:
+            out += ["add hl, sp", f"ld hl, sp+{rng.randrange(-128, 128)}", "inc sp", "dec sp"]
+        elif k < 0.66:
+            e = rng.randrange(1, 100)
+            out += [f"add sp, {e}", f"add sp, {-e}"]
+        elif k < 0.67:
+            out.append(f"ld [${0xC000 + rng.randrange(0x800, 0x1800):04x}], sp")
+        elif k < 0.71:
+            p1, p2 = rng.choice(["bc", "de", "hl", "af"]), rng.choice(["bc", "de", "hl", "af"])
+            out += [f"push {p1}", f"pop {p2}"]
+        elif k < 0.74:
+            out.append(f"call {'' if rng.random() < 0.5 else rng.choice(CC) + ', '}sub{rng.randrange(8)}")
+        elif k < 0.76:
+            out.append(f"rst ${rng.choice([0x08, 0x10, 0x18, 0x20, 0x28, 0x30]):02x}")
+        elif k < 0.79:
+            lbl = f"skip_{idx}_{len(out)}"
+            out += [f"jr {rng.choice(CC)}, {lbl}", f"inc {rng.choice(R8)}", f"{lbl}:"]
+        elif k < 0.81:
+            lbl = f"skip_{idx}_{len(out)}"
+            out += [f"jp {rng.choice(CC)}, {lbl}", f"dec {rng.choice(R8)}", f"{lbl}:"]
+        elif k < 0.84:
+            io = rng.choice(IO_W)
+            v = rng.randrange(256)
+            if io == 0x41:
+                v &= 0x78
+            out += [f"ld a, ${v:02x}", f"ldh [${io:02x}], a"]
+        elif k < 0.88:
+            io = rng.choice(IO_R)
+            if io == 0x00:
+                out += [f"ld a, ${rng.choice([0x10, 0x20, 0x30, 0x00]):02x}", "ldh [$00], a", "ldh a, [$00]", "ldh a, [$00]"]
+            else:
+                out.append(f"ldh a, [${io:02x}]")
+            if rng.random() < 0.5:
+                lbl = f"jj_{idx}_{len(out)}"
+                out += [f"bit {rng.randrange(8)}, a", f"jr z, {lbl}", f"inc {rng.choice(['b', 'c', 'd', 'e'])}", f"{lbl}:"]
+        elif k < 0.89:
+            out += [f"ld c, ${rng.choice(IO_R):02x}", "ld a, [c]" if rng.random() < 0.5 else "ld [c], a"]
+            if out[-1] == "ld [c], a":
+                out[-2] = f"ld c, ${rng.choice([0x42, 0x43, 0x47, 0x4a, 0x90]):02x}"
+        elif k < 0.905:
+            out.append("halt")
+        elif k < 0.915:
+            out.append(rng.choice(["di", "ei", "ei"]))
+        elif k < 0.93:
+            b = rng.randrange(1, n_banks)
+            out += [f"ld a, ${b:02x}", "ld [$2100], a", f"call ${0x4000 + 0x10 * rng.randrange(4):04x}"]
+        elif k < 0.945:
+            out += ["ld a, $0a", "ld [$0000], a", f"ld a, ${rng.randrange(4):02x}", "ld [$4000], a",
+                    f"ld hl, ${0xA000 + rng.randrange(0x2000):04x}", rng.choice(["ld [hl], b", "ld a, [hl]", "inc [hl]"])]
+            if rng.random() < 0.3:
+                out += ["xor a", "ld [$0000], a", "ld a, [hl]"]
+        elif k < 0.955:
+            out += [f"ld a, ${rng.choice([0xC1, 0xC2, 0xC0, 0x80, 0x00, 0xFE]):02x}", "call $ff80"]
+        elif k < 0.96:
+            out.append("nop")
+        elif k < 0.975:
+            out += [f"ld a, ${rng.randrange(256):02x}", f"ldh [${rng.choice([0x07, 0x06, 0x05, 0x04]):02x}], a"]
+        else:
+            out.append(f"ld {rng.choice(['bc', 'de'])}, ${rng.randrange(65536):04x}")
+    return out
+
+
+def fuzz_source(seed: int, n_blocks: int = 160, n_banks: int = 8) -> str:
+    rng = random.Random(seed)
+    L = ["section 0"]
+    for v in range(8):
+        L += [f"org ${v * 8:04x}", "inc e" if v else "nop", "ret"]
+    L += ["org $0040", "jp vblank", "org $0048", "jp stat", "org $0050", "jp timer",
+          "org $0058", "reti", "org $0060", "jp joyp"]
+    L += ["org $0100", "nop", "jp start", "org $0150"]
+    L += ["start:", "di", "ld sp, $dff0",
+          # copy the DMA stub to HRAM (pokered's WriteDMACodeToHRAM)
+          "ld hl, dma_stub", "ld de, $ff80", "ld b, 10", ".cp:", "ld a, [hl+]", "ld [de], a", "inc de",
+          "dec b", "jr nz, .cp",
+          f"ld a, ${rng.choice([0x01, 0x03, 0x05, 0x07, 0x11, 0x15, 0x17, 0x1F]):02x}", "ldh [$ff], a",
+          f"ld a, ${rng.choice([0x00, 0x04, 0x05, 0x06, 0x07]):02x}", "ldh [$07], a",
+          f"ld a, ${rng.randrange(154):02x}", "ldh [$45], a",
+          f"ld a, ${rng.choice([0x00, 0x08, 0x20, 0x40, 0x48, 0x10]):02x}", "ldh [$41], a",
+          "ld a, $e3", "ldh [$40], a", "ld a, $e4", "ldh [$47], a", "ld a, $d0", "ldh [$48], a",
+          # tiles / map / OAM buffer with some non-zero content so the PPU has work
+          "ld hl, $8000", "ld bc, $1800", ".t:", "ld a, l", "xor h", "ld [hl+], a", "dec bc", "ld a, b",
+          "or c", "jr nz, .t",
+          "ld hl, $c100", "ld b, 160", ".o:", "ld a, l", "add a, b", "ld [hl+], a", "dec b", "jr nz, .o",
+          "ei", "main:"]
+    for i in range(n_blocks):
+        L += _block(rng, i, n_banks)
+    L += ["jp main"]
+    for s in range(8):
+        L += [f"sub{s}:"] + _block(rng, 1000 + s, n_banks, max_n=5) + ["ret"]
+    L += ["vblank:", "push af", "push hl", "ld hl, $c0f0", "inc [hl]", "ldh a, [$44]", "ld [$c0f1], a",
+          "ld a, $c1", "call $ff80",
+          # every 32nd vblank: LCD off for a short while (pokered's DisableLCD/EnableLCD pattern)
+          "ld a, [$c0f0]", "and $1f", "jr nz, vb_done", "ldh a, [$40]", "and $7f", "ldh [$40], a",
+          "ld h, $20", "vb_wait:", "dec h", "jr nz, vb_wait", "ldh a, [$40]", "or $80", "ldh [$40], a",
+          "vb_done:", "pop hl", "pop af", "reti",
+          "stat:", "push af", "ldh a, [$41]", "ld [$c0f2], a", "ldh a, [$04]", "ldh [$43], a", "pop af", "reti",
+          "timer:", "push af", "ld a, [$c0f3]", "inc a", "ld [$c0f3], a", "pop af", "reti",
+          "joyp:", "push af", "ld a, $10", "ldh [$00], a", "ldh a, [$00]", "ld [$c0f4], a", "pop af", "reti",
+          "dma_stub:", "db $3e, $c3, $e0, $46, $3e, $28, $3d, $20, $fd, $c9"]
+    # the stub writes a fixed page; patch: use A as the page (ld a,N removed): ldh [$46],a ; wait ; ret
+    L[-1] = "db $e0, $46, $3e, $28, $3d, $20, $fd, $c9, $00, $00"
+    for b in range(1, n_banks):
+        L += [f"section {b}"]
+        for j in range(4):
+            L += [f"org ${0x4000 + 0x10 * j:04x}", f"ld a, ${b:02x}", f"add a, {rng.choice(R8)}", f"ld [${0xC080 + b:04x}], a",
+                  "ld a, $01", "ld [$2100], a", "ret"]
+    return "\n".join(L)
+
+
+def fuzz_rom(seed: int, n_blocks: int = 160, n_banks: int = 8) -> bytes:
+    return build_rom(fuzz_source(seed, n_blocks, n_banks), n_banks=n_banks, title=f"FUZZ{seed}")

@@ -1,0 +1,71 @@
+"""HIP kernel vs the CPU oracle, bit-exact on the whole machine state.
+
+Every env's state after K env-steps is exported from the device as a PyBoy v9 savestate
+(pk_snapshot) and compared byte-for-byte with the oracle's own v9 export (CPU registers, IME/HALT,
+IE/IF, VRAM, OAM, LCD registers and clocks, per-line scroll params, the 144x160 screen, WRAM,
+HRAM, IO, timer, MBC registers, cartridge SRAM)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+from pokegym_amd.testrom.fuzz import fuzz_rom
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _diff(a: bytes, b: bytes):
+    a = np.frombuffer(a, np.uint8)
+    b = np.frombuffer(b, np.uint8)
+    idx = np.nonzero(a != b)[0]
+    return idx[:12].tolist()
+
+
+def _run_both(rom, state, n, steps, seed, render=True):
+    import torch
+    from pokegym_amd.emulator import BatchedEmulator
+    rng = np.random.default_rng(seed)
+    actions = rng.integers(0, 9, size=(steps, n), dtype=np.uint8)
+    emu = BatchedEmulator(rom, n, state=state, render=render)
+    for s in range(steps):
+        emu.step(torch.from_numpy(actions[s]).to(emu.device))
+    torch.cuda.synchronize()
+    gpu = [emu.snapshot(e) for e in range(n)]
+    ref, _ = oracle.batch_run(rom, state, actions, want_screens=False)
+    emu.close()
+    return gpu, ref
+
+
+@pytest.mark.parametrize("seed", [0, 1, 3, 4, 6, 8, 9, 11])
+def test_fuzz_rom_parity(seed):
+    rom = fuzz_rom(seed)
+    n, steps = 128, 12
+    gpu, ref = _run_both(rom, None, n, steps, seed)
+    bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
+    assert not bad, bad[:4]
+
+
+def test_bulbasaur_state_parity():
+    """Start from the reference's Bulbasaur.state (Oak's lab) under a fuzz ROM."""
+    st = open(os.path.join(os.path.dirname(GOLD), "..", "pokegym_amd", "states", "Bulbasaur.state"), "rb").read()
+    rom = fuzz_rom(21)
+    n, steps = 64, 10
+    gpu, ref = _run_both(rom, st, n, steps, 5)
+    bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
+    assert not bad, bad[:4]
+
+
+def test_load_snapshot_roundtrip():
+    import torch
+    from pokegym_amd.emulator import BatchedEmulator
+    z = np.load(os.path.join(GOLD, "states.npz"))
+    rom = fuzz_rom(2)
+    emu = BatchedEmulator(rom, 70)
+    for i, st in enumerate(z["states"]):
+        emu.load_env(65 - i, st.tobytes())
+    torch.cuda.synchronize()
+    for i, st in enumerate(z["states"]):
+        assert emu.snapshot(65 - i) == st.tobytes()
+    emu.close()
