@@ -85,6 +85,12 @@ int pk_load_env(pk_handle* h, uint32_t env, const uint8_t* host_v9, uint64_t len
 /* Emulated instructions executed by the last pk_step, summed over envs (synchronous). */
 int pk_last_instr_count(pk_handle* h, uint64_t* out);
 
+/* Kernel timing with HIP events recorded on the step's stream around K1 (emulate) and K2
+ * (render) of every pk_step while enabled.  pk_profile_read synchronises, returns the summed
+ * milliseconds and the number of profiled steps since the last read, and resets the sums. */
+int pk_profile_enable(pk_handle* h, int on);
+int pk_profile_read(pk_handle* h, double* emulate_ms, double* render_ms, uint64_t* steps);
+
 #ifdef __cplusplus
 }
 #endif

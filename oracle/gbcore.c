@@ -7,9 +7,11 @@
  * behaviour each block restates. Savestate v9 layout: SURVEY.md §5 (pinned on 264 reference files).
  * Parity of CPU trajectories vs PyBoy is UNPINNED (no PyBoy, no ROM, no recorded trajectories).
  */
+#define _POSIX_C_SOURCE 199309L
 #include "gbcore.h"
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #define FRAME_CYCLES 70224u
 #define INTR_VBLANK 0x01
@@ -942,4 +944,33 @@ int gb_batch_run(const uint8_t* rom, uint32_t rom_len, const uint8_t* state, uin
     }
     gb_free(tmpl);
     return 0;
+}
+
+/* CPU baseline ("port"): n envs, `warmup` untimed env-steps, then `steps` timed env-steps with
+ * uniform random actions 0..7 from a counter-based hash of (seed, env, t).  Single thread.
+ * Returns elapsed seconds of the timed part; *instr_out = emulated instructions in it. */
+double gb_bench(const uint8_t* rom, uint32_t rom_len, const uint8_t* state, uint32_t state_len,
+                uint32_t n, uint32_t warmup, uint32_t steps, uint32_t seed, uint64_t* instr_out) {
+    gb_t* tmpl = gb_new(rom, rom_len);
+    if (!tmpl) return -1.0;
+    if (state && gb_load_state(tmpl, state, state_len)) { gb_free(tmpl); return -2.0; }
+    gb_t** envs = (gb_t**)calloc(n, sizeof(gb_t*));
+    for (uint32_t e = 0; e < n; e++) envs[e] = gb_clone(tmpl);
+    #define ACT(e, t) ((int)((((uint64_t)(seed) * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)(e) * 0xBF58476D1CE4E5B9ull) ^ ((uint64_t)(t) * 0x94D049BB133111EBull)) >> 61))
+    for (uint32_t t = 0; t < warmup; t++)
+        for (uint32_t e = 0; e < n; e++) gb_run_action(envs[e], ACT(e, t), 24, 8);
+    uint64_t i0 = 0;
+    for (uint32_t e = 0; e < n; e++) i0 += envs[e]->instr_count;
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    for (uint32_t t = warmup; t < warmup + steps; t++)
+        for (uint32_t e = 0; e < n; e++) gb_run_action(envs[e], ACT(e, t), 24, 8);
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    uint64_t i1 = 0;
+    for (uint32_t e = 0; e < n; e++) { i1 += envs[e]->instr_count; gb_free(envs[e]); }
+    #undef ACT
+    free(envs);
+    gb_free(tmpl);
+    if (instr_out) *instr_out = i1 - i0;
+    return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
 }

@@ -60,6 +60,9 @@ def lib():
         L.gb_render_from_state.argtypes = [u8p, ctypes.c_uint32, u8p]
         L.gb_batch_run.argtypes = [u8p, ctypes.c_uint32, u8p, ctypes.c_uint32, ctypes.c_uint32,
                                    ctypes.c_uint32, u8p, ctypes.c_int, u8p, u8p]
+        L.gb_bench.restype = ctypes.c_double
+        L.gb_bench.argtypes = [u8p, ctypes.c_uint32, u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                               ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]
         _lib = L
     return _lib
 
@@ -163,3 +166,15 @@ def batch_run(rom: bytes, state: bytes | None, actions: np.ndarray, want_states=
     if rc:
         raise ValueError(f"gb_batch_run failed: {rc}")
     return so, sc
+
+
+def bench(rom: bytes, state: bytes | None, n: int, warmup: int, steps: int, seed: int):
+    """Single-thread CPU timing of the oracle: returns (seconds, emulated_instructions)."""
+    r = np.frombuffer(rom, dtype=np.uint8).copy()
+    st = np.frombuffer(state, dtype=np.uint8).copy() if state is not None else None
+    ic = ctypes.c_uint64()
+    sec = lib().gb_bench(_ptr(r), len(r), _ptr(st) if st is not None else None,
+                         len(st) if st is not None else 0, n, warmup, steps, seed, ctypes.byref(ic))
+    if sec < 0:
+        raise ValueError("gb_bench failed")
+    return sec, int(ic.value)

@@ -18,7 +18,7 @@ ROWS, COLS = 144, 160
 # the exported symbols declared in include/pokegym_amd.h
 EXPORTS = ("pk_create", "pk_destroy", "pk_last_error", "pk_abi_version", "pk_reset", "pk_step",
            "pk_screen_ptr", "pk_num_envs", "pk_peek", "pk_poke", "pk_snapshot", "pk_load_env",
-           "pk_last_instr_count")
+           "pk_last_instr_count", "pk_profile_enable", "pk_profile_read")
 
 
 class PkConfig(ctypes.Structure):
@@ -69,6 +69,9 @@ def load(path: str = LIB_PATH):
     L.pk_snapshot.argtypes = [vp, ctypes.c_uint32, u8p, ctypes.c_uint64]
     L.pk_load_env.argtypes = [vp, ctypes.c_uint32, u8p, ctypes.c_uint64]
     L.pk_last_instr_count.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
+    L.pk_profile_enable.argtypes = [vp, ctypes.c_int]
+    dp = ctypes.POINTER(ctypes.c_double)
+    L.pk_profile_read.argtypes = [vp, dp, dp, ctypes.POINTER(ctypes.c_uint64)]
     _lib = L
     return L
 

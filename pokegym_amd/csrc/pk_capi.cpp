@@ -226,7 +226,21 @@ struct pk_handle {
     uint8_t* scratch = nullptr;  // PK_PHYS staging for one env
     size_t lat_stride = 0;
     Template tmpl;
+    // profiling: 3 events per profiled step (start, after K1, after K2)
+    bool prof = false;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
 };
+
+static int prof_event(pk_handle* h, hipStream_t s) {
+    if (h->ev_used == h->ev_pool.size()) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        h->ev_pool.push_back(e);
+    }
+    HIPCHK(hipEventRecord(h->ev_pool[h->ev_used++], s));
+    return 0;
+}
 
 extern "C" {
 
@@ -238,6 +252,7 @@ uint32_t pk_num_envs(const pk_handle* h) { return h ? h->n : 0; }
 void pk_destroy(pk_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
+    for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     void* ptrs[] = {h->mem, h->regs, h->lat, h->screen, h->rom, h->dtab, h->t_mem, h->t_regs,
                     h->t_lat, h->t_screen, h->scratch};
     for (void* p : ptrs)
@@ -343,8 +358,12 @@ int pk_step(pk_handle* h, const uint8_t* actions, uint8_t* screen_out, double* r
     a.rom_bank_mask = h->bank_mask; a.mbc = h->mbc; a.frames = h->frames;
     a.release_frame = h->release; a.render_last = (h->flags & PK_F_RENDER) ? 1 : 0;
     a.lat_stride = (uint32_t)h->lat_stride;
+    int rc;
+    if (h->prof && (rc = prof_event(h, s))) return rc;
     HIPCHK(pk_launch_step(a, s));
+    if (h->prof && (rc = prof_event(h, s))) return rc;
     if (a.render_last) HIPCHK(pk_launch_render(a, s));
+    if (h->prof && (rc = prof_event(h, s))) return rc;
     if (screen_out)
         HIPCHK(hipMemcpyAsync(screen_out, h->screen, (size_t)h->n * PK_SCREEN, hipMemcpyDeviceToDevice, s));
     if (rew || term || trunc)
@@ -500,6 +519,32 @@ int pk_poke(pk_handle* h, uint32_t env, uint16_t addr, uint32_t len, const uint8
         HIPCHK(hipMemcpy(h->mem + (size_t)gid * PK_GROUP_STRIDE + (size_t)phys * PK_LANES + lane, &in[i], 1,
                          hipMemcpyHostToDevice));
     }
+    return 0;
+}
+
+int pk_profile_enable(pk_handle* h, int on) {
+    if (!h) return fail(-EINVAL, "null handle");
+    h->prof = on != 0;
+    return 0;
+}
+
+int pk_profile_read(pk_handle* h, double* emu_ms, double* render_ms, uint64_t* steps) {
+    if (!h || !emu_ms || !render_ms || !steps) return fail(-EINVAL, "null argument");
+    HIPCHK(hipSetDevice(h->device));
+    double a = 0, b = 0;
+    size_t n = h->ev_used / 3;
+    if (n) HIPCHK(hipEventSynchronize(h->ev_pool[h->ev_used - 1]));
+    for (size_t i = 0; i < n; i++) {
+        float t1 = 0, t2 = 0;
+        HIPCHK(hipEventElapsedTime(&t1, h->ev_pool[3 * i], h->ev_pool[3 * i + 1]));
+        HIPCHK(hipEventElapsedTime(&t2, h->ev_pool[3 * i + 1], h->ev_pool[3 * i + 2]));
+        a += t1;
+        b += t2;
+    }
+    *emu_ms = a;
+    *render_ms = b;
+    *steps = n;
+    h->ev_used = 0;
     return 0;
 }
 

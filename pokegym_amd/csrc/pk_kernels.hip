@@ -206,21 +206,32 @@ __device__ void render_line(const Mem& m, u32 y, u32 lat0, u32 lat1, int lw, u8*
     }
 }
 
-// rasterise every latched-but-pending line of this lane now (before VRAM/OAM changes)
-__device__ __noinline__ void flush_lines(const PkStepArgs& A, const Mem& m, u32 env, u32 gid, Lane& L) {
-    u32* lat0 = A.lat;
-    u32* lat1 = A.lat + A.lat_stride;
-    u32* lat2 = A.lat + 2u * A.lat_stride;
+// rasterise every latched-but-pending line of this lane now (before VRAM/OAM change).  Rare
+// path: kept out of line with by-value arguments so the hot loop's lane state stays in VGPRs.
+__device__ __noinline__ void flush_lines(u32* lat, u32 lat_stride, u8* screen, u8* gbase, u32 lane, u32 env, u32 gid) {
+    Mem m;
+    m.g = gbase;
+    m.lane = lane;
+    u32* lat0 = lat;
+    u32* lat1 = lat + lat_stride;
+    u32* lat2 = lat + 2u * lat_stride;
     for (u32 y = 0; y < PK_ROWS; y++) {
-        u32 idx = (gid * PK_ROWS + y) * PK_LANES + m.lane;
+        u32 idx = (gid * PK_ROWS + y) * PK_LANES + lane;
         u32 l2 = lat2[idx];
         if (l2 & 0x100u) {
-            render_line(m, y, lat0[idx], lat1[idx], (int)(l2 & 0xFFu) - 1, A.screen + (size_t)env * PK_SCREEN + y * PK_COLS);
+            render_line(m, y, lat0[idx], lat1[idx], (int)(l2 & 0xFFu) - 1, screen + (size_t)env * PK_SCREEN + y * PK_COLS);
             lat2[idx] = l2 & ~0x100u;
         }
     }
-    L.npend = 0;
 }
+
+#define FLUSH_PENDING()                                                                   \
+    do {                                                                                  \
+        if (L.npend) {                                                                    \
+            flush_lines(A.lat, A.lat_stride, A.screen, m.g, m.lane, env, gid);            \
+            L.npend = 0;                                                                  \
+        }                                                                                 \
+    } while (0)
 
 // ---------------------------------------------------------------------------------------------
 // LCD tick (pyboy lcd.py LCD.tick) — oracle: gbcore.c lcd_tick
@@ -353,7 +364,7 @@ __device__ __forceinline__ u32 rom_read(const PkStepArgs& A, const u8* lds_bank0
     return A.rom[bank * 0x4000u + (a - 0x4000u)];
 }
 
-__device__ u32 io_read_special(const Lane& L, u32 a) {
+__device__ __forceinline__ u32 io_read_special(const Lane& L, u32 a) {
     switch (a) {
         case 0xFF04: return bfe8(L.tim0, 0);
         case 0xFF05: return bfe8(L.tim0, 8);
@@ -404,7 +415,7 @@ __device__ __forceinline__ u32 bus_read(const PkStepArgs& A, const u8* lds_bank0
     return ld_phys(m, phys);
 }
 
-__device__ __noinline__ void lcd_set_lcdc(Lane& L, u32 v) {
+__device__ __forceinline__ void lcd_set_lcdc(Lane& L, u32 v) {
     L.lcd0 = setb8(L.lcd0, 0, v);
     if (!(v & 0x80u)) {
         L.clock = 0;
@@ -415,18 +426,17 @@ __device__ __noinline__ void lcd_set_lcdc(Lane& L, u32 v) {
     }
 }
 
-__device__ void bus_write(const PkStepArgs& A, const u8* lds_bank0, const Mem& m, Lane& L, u32 env, u32 gid, u32 a, u32 v);
 
-__device__ __noinline__ void oam_dma(const PkStepArgs& A, const u8* lds_bank0, const Mem& m, Lane& L, u32 env, u32 gid, u32 v) {
+__device__ __forceinline__ void oam_dma(const PkStepArgs& A, const u8* lds_bank0, const Mem& m, Lane& L, u32 env, u32 gid, u32 v) {
     u32 src = v << 8;
-    if (L.npend) flush_lines(A, m, env, gid, L);
+    FLUSH_PENDING();
     for (u32 n = 0; n < 0xA0u; n++) {
         u32 b = bus_read(A, lds_bank0, m, L, (src + n) & 0xFFFFu);
         st_phys(m, PK_P_OAM + n, b);
     }
 }
 
-__device__ __noinline__ void io_write_special(const PkStepArgs& A, const u8* lds_bank0, const Mem& m, Lane& L, u32 env, u32 gid, u32 a, u32 v) {
+__device__ __forceinline__ void io_write_special(const PkStepArgs& A, const u8* lds_bank0, const Mem& m, Lane& L, u32 env, u32 gid, u32 a, u32 v) {
     switch (a) {
         case 0xFF04: L.tim0 = setb8(L.tim0, 0, 0u); L.tim1 = 0u; break;
         case 0xFF05: L.tim0 = setb8(L.tim0, 8, v); break;
@@ -462,11 +472,11 @@ __device__ __forceinline__ void mbc_write(const PkStepArgs& A, Lane& L, u32 a, u
     }
 }
 
-__device__ void bus_write(const PkStepArgs& A, const u8* lds_bank0, const Mem& m, Lane& L, u32 env, u32 gid, u32 a, u32 v) {
+__device__ __forceinline__ void bus_write(const PkStepArgs& A, const u8* lds_bank0, const Mem& m, Lane& L, u32 env, u32 gid, u32 a, u32 v) {
     if (a < 0x8000u) { mbc_write(A, L, a, v); return; }
     u32 phys;
     if (a < 0xA000u) {
-        if (L.npend) flush_lines(A, m, env, gid, L);
+        FLUSH_PENDING();
         phys = PK_P_VRAM + (a - 0x8000u);
     } else if (a < 0xC000u) {
         if (A.mbc == 0u || !bfe8(L.mbc, 16)) return;
@@ -474,7 +484,7 @@ __device__ void bus_write(const PkStepArgs& A, const u8* lds_bank0, const Mem& m
     } else if (a < 0xFE00u) {
         phys = PK_P_WRAM + (a & 0x1FFFu);
     } else if (a < 0xFF00u) {
-        if (a < 0xFEA0u && L.npend) flush_lines(A, m, env, gid, L);
+        if (a < 0xFEA0u) FLUSH_PENDING();
         phys = PK_P_OAM + (a - 0xFE00u);
     } else if (a >= 0xFF80u) {
         if (a == 0xFFFFu) { S_IE(L, v); return; }
@@ -493,24 +503,37 @@ __device__ void bus_write(const PkStepArgs& A, const u8* lds_bank0, const Mem& m
 
 // ---------------------------------------------------------------------------------------------
 // register file helpers (W0 = C|B<<8|E<<16|D<<24, W1 = L|H<<8|A<<16|F<<24)
+// NOTE: selections between lane-state fields are written as arithmetic on VALUES. A C++
+// `cond ? L.w1 : L.w0` (or an if/else storing to one of two fields) lets LLVM form a select of
+// field ADDRESSES, which forces the whole Lane struct into scratch memory.
 __device__ __forceinline__ u32 rd8(const Lane& L, u32 r) {
-    u32 w = (r & 4u) ? L.w1 : L.w0;
+    const u32 sel = 0u - ((r >> 2) & 1u);
+    const u32 w = (L.w0 & ~sel) | (L.w1 & sel);
     return bfe8(w, ((r ^ 1u) & 3u) * 8u);
 }
 __device__ __forceinline__ void wr8(Lane& L, u32 r, u32 v) {
-    u32 sh = ((r ^ 1u) & 3u) * 8u;
-    if (r & 4u) L.w1 = setb8(L.w1, sh, v);
-    else L.w0 = setb8(L.w0, sh, v);
+    const u32 sh = ((r ^ 1u) & 3u) * 8u;
+    const u32 sel = 0u - ((r >> 2) & 1u);
+    const u32 msk = 0xFFu << sh, nv = (v & 0xFFu) << sh;
+    const u32 w0 = L.w0, w1 = L.w1;
+    L.w0 = (w0 & ~(msk & ~sel)) | (nv & ~sel);
+    L.w1 = (w1 & ~(msk & sel)) | (nv & sel);
 }
 __device__ __forceinline__ u32 rd16(const Lane& L, u32 p) {  // BC DE HL SP
-    return p == 0u ? (L.w0 & 0xFFFFu) : p == 1u ? (L.w0 >> 16) : p == 2u ? (L.w1 & 0xFFFFu) : L.sp;
+    const u32 w0 = L.w0, w1 = L.w1, sp = L.sp;
+    const u32 lo = (p & 1u) ? (w0 >> 16) : (w0 & 0xFFFFu);
+    const u32 hi = (p & 1u) ? sp : (w1 & 0xFFFFu);
+    return (p & 2u) ? hi : lo;
 }
 __device__ __forceinline__ void wr16(Lane& L, u32 p, u32 v) {
     v &= 0xFFFFu;
-    if (p == 0u) L.w0 = (L.w0 & 0xFFFF0000u) | v;
-    else if (p == 1u) L.w0 = (L.w0 & 0xFFFFu) | (v << 16);
-    else if (p == 2u) L.w1 = (L.w1 & 0xFFFF0000u) | v;
-    else L.sp = v;
+    const u32 w0 = L.w0, w1 = L.w1, sp = L.sp;
+    const u32 n0 = p == 0u ? ((w0 & 0xFFFF0000u) | v) : p == 1u ? ((w0 & 0xFFFFu) | (v << 16)) : w0;
+    const u32 n1 = p == 2u ? ((w1 & 0xFFFF0000u) | v) : w1;
+    const u32 ns = p == 3u ? v : sp;
+    L.w0 = n0;
+    L.w1 = n1;
+    L.sp = ns;
 }
 #define A_(L) bfe8((L).w1, 16)
 #define F_(L) bfe8((L).w1, 24)

@@ -109,6 +109,15 @@ class BatchedEmulator:
         check(self._L.pk_last_instr_count(self._h, ctypes.byref(v)), "pk_last_instr_count")
         return int(v.value)
 
+    def profile_enable(self, on: bool = True):
+        check(self._L.pk_profile_enable(self._h, 1 if on else 0), "pk_profile_enable")
+
+    def profile_read(self):
+        """(emulate_ms_total, render_ms_total, steps) since the last read (synchronous)."""
+        a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
+        check(self._L.pk_profile_read(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)), "pk_profile_read")
+        return a.value, b.value, int(n.value)
+
     def close(self):
         if getattr(self, "_h", None):
             torch.cuda.synchronize(self.device)
