@@ -67,6 +67,8 @@ def main():
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--workload", choices=["config3", "config2"], default="config3",
                     help="config3: rendered screen obs + random actions; config2: headless, fixed action cycle")
+    ap.add_argument("--actions", choices=["auto", "random", "same"], default="auto",
+                    help="override the workload's action stream (diagnostics)")
     ap.add_argument("--rom", default=None)
     ap.add_argument("--state", default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -98,7 +100,11 @@ def main():
     n = args.envs
     emu = BatchedEmulator(rom, n, state=state, device=local, render=render)
     total = args.warmup + args.steps
-    if args.workload == "config3":
+    if args.actions == "same":
+        g = torch.Generator(device=dev)
+        g.manual_seed(1234 + rank)
+        acts = torch.randint(0, 8, (total, 1), generator=g, device=dev).to(torch.uint8).expand(total, n).contiguous()
+    elif args.workload == "config3" or args.actions == "random":
         g = torch.Generator(device=dev)
         g.manual_seed(1234 + rank)   # Philox counter-based RNG on the device
         acts = torch.randint(0, 8, (total, n), generator=g, device=dev, dtype=torch.int64).to(torch.uint8)

@@ -54,7 +54,7 @@ struct gb {
     uint8_t directional, standard;
     /* header bytes 1..4 of the state file */
     uint8_t hdr[4];
-    uint64_t instr_count, frame_count;
+    uint64_t instr_count, frame_count, iter_count;
 };
 
 static const uint32_t TIMER_DIVIDERS[4] = {1024, 16, 64, 256};
@@ -547,11 +547,27 @@ static uint32_t exec_cb(gb_t* gb, uint8_t op) {
     return cyc;
 }
 
+/* optional instruction trace (debugging/tests): pc, BC|DE<<16, HL|A<<16|F<<24, SP, opcode */
+static uint32_t* g_trace = NULL;
+static uint64_t g_trace_cap = 0, g_trace_n = 0;
+void gb_trace_enable(uint32_t* buf, uint64_t cap) { g_trace = buf; g_trace_cap = cap; g_trace_n = 0; }
+uint64_t gb_trace_count(void) { return g_trace_n; }
+
 /* cpu.fetch_and_execute + opcodes.py; returns T-cycles */
 static uint32_t cpu_execute(gb_t* gb) {
     uint16_t pc = gb->PC;
     uint8_t op = RD(pc);
     gb->instr_count++;
+    if (g_trace && g_trace_n < g_trace_cap) {
+        uint32_t* r = g_trace + g_trace_n * 6;
+        r[0] = pc;
+        r[1] = (uint32_t)(gb->C | (gb->B << 8) | (gb->E << 16) | ((uint32_t)gb->D << 24));
+        r[2] = (uint32_t)((gb->HL & 0xFF) | ((gb->HL >> 8) << 8) | (gb->A << 16) | ((uint32_t)gb->F << 24));
+        r[3] = gb->SP;
+        r[4] = op;
+        r[5] = 0;
+        g_trace_n++;
+    }
     if (op == 0xCB) return exec_cb(gb, RD((uint16_t)(pc + 1)));
     uint8_t n8 = 0;
     uint16_t n16 = 0;
@@ -757,6 +773,7 @@ void gb_tick(gb_t* gb) {
         if (timer_tick(gb, (uint32_t)cycles)) gb->IF |= INTR_TIMER;
         gb->IF |= lcd_tick(gb, (uint32_t)cycles);
         budget += (uint32_t)cycles + 1u;
+        gb->iter_count++;
         if (budget > PK_FRAME_BUDGET) gb->frame_done = 1;
     } while (!gb->frame_done);
     gb->frame_done = 0;
@@ -901,6 +918,7 @@ const uint8_t* gb_screen_shades(const gb_t* gb) { return (const uint8_t*)gb->scr
 const uint8_t* gb_wram(const gb_t* gb) { return gb->wram; }
 uint64_t gb_instr_count(const gb_t* gb) { return gb->instr_count; }
 uint64_t gb_frame_count(const gb_t* gb) { return gb->frame_count; }
+uint64_t gb_iter_count(const gb_t* gb) { return gb->iter_count; }
 int gb_crashed(const gb_t* gb) { return gb->crashed; }
 
 int gb_render_from_state(const uint8_t* state, uint32_t len, uint8_t* out) {

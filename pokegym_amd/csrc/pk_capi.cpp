@@ -9,6 +9,7 @@
 #include <errno.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -218,12 +219,16 @@ struct pk_handle {
     uint32_t* lat = nullptr;
     uint8_t* screen = nullptr;
     uint8_t* rom = nullptr;
+    pk_rom_entry* rom16 = nullptr;
     uint32_t* dtab = nullptr;
     uint8_t* t_mem = nullptr;
     uint32_t* t_regs = nullptr;
     uint32_t* t_lat = nullptr;
     uint8_t* t_screen = nullptr;
     uint8_t* scratch = nullptr;  // PK_PHYS staging for one env
+    int8_t* bank_slot = nullptr;  // [128] LDS slot per ROM bank (-1 = global)
+    uint8_t* slot_bank = nullptr; // [PK_LDS_SLOTS]
+    uint32_t nslots = 1;
     size_t lat_stride = 0;
     Template tmpl;
     // profiling: 3 events per profiled step (start, after K1, after K2)
@@ -253,7 +258,7 @@ void pk_destroy(pk_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
-    void* ptrs[] = {h->mem, h->regs, h->lat, h->screen, h->rom, h->dtab, h->t_mem, h->t_regs,
+    void* ptrs[] = {h->mem, h->regs, h->lat, h->screen, h->rom, h->rom16, h->bank_slot, h->slot_bank, h->dtab, h->t_mem, h->t_regs,
                     h->t_lat, h->t_screen, h->scratch};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -307,18 +312,40 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     ALLOC(h->lat, 3 * h->lat_stride * 4);
     ALLOC(h->screen, (size_t)h->npad * PK_SCREEN);
     ALLOC(h->rom, cfg->rom_len);
-    ALLOC(h->dtab, 512 * 4);
+    ALLOC(h->rom16, cfg->rom_len * sizeof(pk_rom_entry));
+    ALLOC(h->dtab, 1024 * 4);
+    ALLOC(h->bank_slot, 128);
+    ALLOC(h->slot_bank, PK_LDS_SLOTS);
     ALLOC(h->t_mem, PK_PHYS);
     ALLOC(h->t_regs, PK_NREGS * 4);
     ALLOC(h->t_lat, 3 * PK_ROWS * 4);
     ALLOC(h->t_screen, PK_SCREEN);
     ALLOC(h->scratch, PK_PHYS + PK_NREGS * 4 + 3 * PK_ROWS * 4 + PK_SCREEN);
 #undef ALLOC
-    uint32_t dt[512];
-    pk_build_decode(dt);
+    uint32_t dt[1024];
+    pk_build_dtab(dt);
+    std::vector<pk_rom_entry> rom16(cfg->rom_len);
+    pk_build_rom16(cfg->rom, (uint32_t)cfg->rom_len, dt, rom16.data());
     hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = hipMemcpy(h->rom16, rom16.data(), rom16.size() * sizeof(pk_rom_entry), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->rom, cfg->rom, cfg->rom_len, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->dtab, dt, sizeof dt, hipMemcpyHostToDevice);
+    {
+        // ROM banks staged in LDS by the step kernel: bank 0 and the first banks after it
+        // (override the count with PK_LDS_SLOTS=1..6 for experiments)
+        uint32_t want = PK_LDS_SLOTS;
+        if (const char* ev = getenv("PK_LDS_SLOTS")) want = (uint32_t)atoi(ev);
+        if (want < 1) want = 1;
+        if (want > PK_LDS_SLOTS) want = PK_LDS_SLOTS;
+        if (want > banks) want = banks;
+        int8_t bs[128];
+        uint8_t sb[PK_LDS_SLOTS] = {0};
+        memset(bs, -1, sizeof bs);
+        for (uint32_t k = 0; k < want; k++) { sb[k] = (uint8_t)k; bs[k] = (int8_t)k; }
+        h->nslots = want;
+        if (e == hipSuccess) e = hipMemcpy(h->bank_slot, bs, sizeof bs, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(h->slot_bank, sb, sizeof sb, hipMemcpyHostToDevice);
+    }
     if (e == hipSuccess) e = hipMemcpy(h->t_mem, h->tmpl.mem.data(), PK_PHYS, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->t_regs, h->tmpl.regs, sizeof h->tmpl.regs, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->t_lat, h->tmpl.lat, sizeof h->tmpl.lat, hipMemcpyHostToDevice);
@@ -353,11 +380,12 @@ int pk_step(pk_handle* h, const uint8_t* actions, uint8_t* screen_out, double* r
     HIPCHK(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
     PkStepArgs a;
-    a.mem = h->mem; a.rom = h->rom; a.regs = h->regs; a.dtab = h->dtab; a.actions = actions;
+    a.mem = h->mem; a.rom = h->rom; a.rom16 = h->rom16; a.regs = h->regs; a.dtab = h->dtab; a.actions = actions;
     a.lat = h->lat; a.screen = h->screen; a.n = h->n; a.npad = h->npad;
     a.rom_bank_mask = h->bank_mask; a.mbc = h->mbc; a.frames = h->frames;
     a.release_frame = h->release; a.render_last = (h->flags & PK_F_RENDER) ? 1 : 0;
     a.lat_stride = (uint32_t)h->lat_stride;
+    a.nslots = h->nslots; a.bank_slot = h->bank_slot; a.slot_bank = h->slot_bank;
     int rc;
     if (h->prof && (rc = prof_event(h, s))) return rc;
     HIPCHK(pk_launch_step(a, s));

@@ -22,6 +22,12 @@ typedef uint8_t u8;
 
 #define FRAME_CYCLES 70224u
 
+// debug hook: the host-simulation test build (tests/hostsim) defines it to record an instruction
+// trace; the gfx950 build compiles it away.
+#ifndef PK_TRACE
+#define PK_TRACE(env, pc, w0, w1, sp, op) ((void)0)
+#endif
+
 
 
 // ---------------------------------------------------------------------------------------------
@@ -31,7 +37,9 @@ struct Lane {
     u32 cpu;            // ime | halted<<1 | queued<<2 | crashed<<3 | stopped<<4 | IE<<8 | IF<<16
     u32 clock, target;
     u32 lcd0, lcd1, lcd2;
-    u32 tim0, tim1;
+    u32 tim0;           // (DIV byte stale in-kernel) | TIMA<<8 | TMA<<16 | TAC<<24
+    u32 divacc;         // DIV<<8 | DIV_counter  (mod 2^16)
+    u32 timac;          // TIMA_counter
     u32 mbc;
     u32 misc;
     u32 icount;
@@ -234,87 +242,76 @@ __device__ __noinline__ void flush_lines(u32* lat, u32 lat_stride, u8* screen, u
     } while (0)
 
 // ---------------------------------------------------------------------------------------------
-// LCD tick (pyboy lcd.py LCD.tick) — oracle: gbcore.c lcd_tick
+// LCD tick (pyboy lcd.py LCD.tick) — oracle: gbcore.c lcd_tick.  The mode transition is written
+// branch-light: under divergence some lane of the wave transitions on most iterations.
 __device__ __forceinline__ u32 lcd_tick(const PkStepArgs& A, Lane& L, u32 gid, u32 lane, u32 cycles) {
     u32 intr = 0;
     L.clock += cycles;
-    u32 lcdc = G_LCDC(L);
+    const u32 lcdc = G_LCDC(L);
     if (lcdc & 0x80u) {
         if (L.clock >= L.target) {
-            u32 nmode = bfe8(L.lcd2, 24);
-            intr |= stat_set_mode(L, nmode);
-            u32 mode = G_STAT(L) & 3u;
+            const u32 nm = bfe8(L.lcd2, 24);
+            u32 stat = G_STAT(L);
+            const bool changed = (stat & 3u) != nm;
+            stat = (stat & 0xFCu) | nm;
+            if (changed && nm != 3u && (stat & (1u << (nm + 3u)))) intr |= 2u;
             u32 ly = G_LY(L);
-            if (mode == 2u) {
-                if (ly == 153u) {
-                    ly = 0;
-                    L.clock %= FRAME_CYCLES;
-                    L.target %= FRAME_CYCLES;
-                } else {
-                    ly += 1u;
-                }
-                L.lcd0 = setb8(L.lcd0, 16, ly);
-                L.target += 80u;
-                L.lcd2 = setb8(L.lcd2, 24, 3u);
-                intr |= stat_update_lyc(L);
-            } else if (mode == 3u) {
-                L.target += 170u;
-                L.lcd2 = setb8(L.lcd2, 24, 0u);
-            } else if (mode == 0u) {
-                L.target += 206u;
-                if (L.render && ly < PK_ROWS) {
-                    // latch this scanline's registers; rasterised by K2 (or flush_lines)
-                    u32 lcd1 = L.lcd1;
-                    u32 wy = bfe8(lcd1, 16), wx = bfe8(lcd1, 24);
-                    int lw = (int)bfe8(L.misc, 16) - 1;
-                    if ((lcdc & 0x20u) && wy <= ly && (int)wx - 7 < (int)PK_COLS) lw += 1;
-                    u32 idx = (gid * PK_ROWS + ly) * PK_LANES + lane;
-                    A.lat[idx] = lcdc | (bfe8(lcd1, 8) << 8) | (bfe8(lcd1, 0) << 16) | (wx << 24);
-                    A.lat[A.lat_stride + idx] = wy | ((L.lcd2 & 0xFFFFFFu) << 8);
-                    A.lat[2u * A.lat_stride + idx] = (u32)(lw + 1) | 0x100u;
-                    if (ly == PK_ROWS - 1u) lw = -1;
-                    L.misc = setb8(L.misc, 16, (u32)(lw + 1));
-                    L.npend += 1u;
-                }
-                L.lcd2 = setb8(L.lcd2, 24, (ly < 143u) ? 2u : 1u);
-            } else {
-                L.target += 456u;
-                L.lcd2 = setb8(L.lcd2, 24, 1u);
-                ly += 1u;
-                L.lcd0 = setb8(L.lcd0, 16, ly);
-                intr |= stat_update_lyc(L);
-                if (ly == 144u) {
-                    intr |= 1u;
-                    L.frame_done = 1u;
-                }
-                if (ly == 153u) L.lcd2 = setb8(L.lcd2, 24, 2u);
+            const bool m2 = nm == 2u, m3 = nm == 3u, m0 = nm == 0u, m1 = nm == 1u;
+            const bool wrap = m2 && ly == 153u;
+            if (wrap) {
+                while (L.clock >= FRAME_CYCLES) L.clock -= FRAME_CYCLES;
+                while (L.target >= FRAME_CYCLES) L.target -= FRAME_CYCLES;
+            }
+            ly = wrap ? 0u : ((m2 || m1) ? ly + 1u : ly);
+            L.target += m2 ? 80u : m3 ? 170u : m0 ? 206u : 456u;
+            if (m2 || m1) {  // STATRegister.update_LYC
+                const bool eq = G_LYC(L) == ly;
+                stat = eq ? (stat | 4u) : (stat & 0xFBu);
+                if (eq && (stat & 0x40u)) intr |= 2u;
+            }
+            const u32 nnext = m2 ? 3u : m3 ? 0u : m0 ? (ly < 143u ? 2u : 1u) : (ly == 153u ? 2u : 1u);
+            if (m1 && ly == 144u) {
+                intr |= 1u;
+                L.frame_done = 1u;
+            }
+            L.lcd0 = (L.lcd0 & 0xFF0000FFu) | (stat << 8) | (ly << 16);
+            L.lcd2 = (L.lcd2 & 0x00FFFFFFu) | (nnext << 24);
+            if (m0 && L.render && ly < PK_ROWS) {
+                // latch this scanline's registers; rasterised by K2 (or flush_lines)
+                const u32 lcd1 = L.lcd1;
+                const u32 wy = bfe8(lcd1, 16), wx = bfe8(lcd1, 24);
+                int lw = (int)bfe8(L.misc, 16) - 1;
+                if ((lcdc & 0x20u) && wy <= ly && (int)wx - 7 < (int)PK_COLS) lw += 1;
+                const u32 idx = (gid * PK_ROWS + ly) * PK_LANES + lane;
+                A.lat[idx] = lcdc | (bfe8(lcd1, 8) << 8) | (bfe8(lcd1, 0) << 16) | (wx << 24);
+                A.lat[A.lat_stride + idx] = wy | ((L.lcd2 & 0xFFFFFFu) << 8);
+                A.lat[2u * A.lat_stride + idx] = (u32)(lw + 1) | 0x100u;
+                if (ly == PK_ROWS - 1u) lw = -1;
+                L.misc = setb8(L.misc, 16, (u32)(lw + 1));
+                L.npend += 1u;
             }
         }
-    } else {
-        if (L.clock >= FRAME_CYCLES) {
-            L.frame_done = 1u;
-            L.clock %= FRAME_CYCLES;
-            if (L.render) L.blank = 1u;
-        }
+    } else if (L.clock >= FRAME_CYCLES) {
+        L.frame_done = 1u;
+        while (L.clock >= FRAME_CYCLES) L.clock -= FRAME_CYCLES;
+        if (L.render) L.blank = 1u;
     }
     return intr;
 }
 
-// timer (pyboy timer.py Timer.tick) — oracle: gbcore.c timer_tick
+// timer (pyboy timer.py Timer.tick) — oracle: gbcore.c timer_tick.
+// DIV/DIV_counter are kept as one 16-bit accumulator: DIV_counter += c; DIV += DIV_counter >> 8;
+// both masked to 8 bits  ==  (DIV << 8 | DIV_counter) + c  mod 2^16.
 __device__ __forceinline__ u32 timer_tick(Lane& L, u32 cycles) {
-    u32 divc = (L.tim1 & 0xFFFFu) + cycles;
-    u32 div = (bfe8(L.tim0, 0) + (divc >> 8)) & 0xFFu;
-    divc &= 0xFFu;
+    L.divacc = (L.divacc + cycles) & 0xFFFFu;
+    const u32 tac = bfe8(L.tim0, 24);
     u32 r = 0;
-    u32 tac = bfe8(L.tim0, 24);
-    u32 timac = L.tim1 >> 16;
-    u32 tima = bfe8(L.tim0, 8);
     if (tac & 4u) {
-        timac += cycles;
-        u32 dsh = ((tac & 3u) == 0u) ? 10u : ((tac & 3u) == 1u) ? 4u : ((tac & 3u) == 2u) ? 6u : 8u;
-        u32 d = 1u << dsh;
-        if (timac >= d) {
-            u32 mul = timac >> dsh;
+        u32 timac = L.timac + cycles;
+        const u32 dsh = ((tac & 3u) == 0u) ? 10u : ((tac & 3u) == 1u) ? 4u : ((tac & 3u) == 2u) ? 6u : 8u;
+        u32 tima = bfe8(L.tim0, 8);
+        if (timac >= (1u << dsh)) {
+            const u32 mul = timac >> dsh;
             timac -= mul << dsh;
             tima += mul;
             if (tima > 0xFFu) {
@@ -325,24 +322,23 @@ __device__ __forceinline__ u32 timer_tick(Lane& L, u32 cycles) {
             }
         }
         L.tim0 = setb8(L.tim0, 8, tima);
+        L.timac = timac;
     }
-    L.tim0 = setb8(L.tim0, 0, div);
-    L.tim1 = divc | (timac << 16);
     return r;
 }
 
 __device__ __forceinline__ int timer_cycles_to_interrupt(const Lane& L) {
-    u32 tac = bfe8(L.tim0, 24);
+    const u32 tac = bfe8(L.tim0, 24);
     if (!(tac & 4u)) return 1 << 16;
-    u32 dsh = ((tac & 3u) == 0u) ? 10u : ((tac & 3u) == 1u) ? 4u : ((tac & 3u) == 2u) ? 6u : 8u;
-    return (int)((0x100u - bfe8(L.tim0, 8)) << dsh) - (int)(L.tim1 >> 16);
+    const u32 dsh = ((tac & 3u) == 0u) ? 10u : ((tac & 3u) == 1u) ? 4u : ((tac & 3u) == 2u) ? 6u : 8u;
+    return (int)((0x100u - bfe8(L.tim0, 8)) << dsh) - (int)L.timac;
 }
 
 // joypad (pyboy interaction.py) — oracle: gbcore.c gb_button / joy_pull
 __device__ __forceinline__ void key_event(Lane& L, u32 button, bool pressed) {
-    u32 od = bfe8(L.misc, 0), os = bfe8(L.misc, 8);
+    const u32 od = bfe8(L.misc, 0), os = bfe8(L.misc, 8);
     u32 nd = od, ns = os;
-    u32 bit = 1u << (button & 3u);
+    const u32 bit = 1u << (button & 3u);
     if (button < 4u) nd = pressed ? (nd & ~bit) : (nd | bit);
     else ns = pressed ? (ns & ~bit) : (ns | bit);
     L.misc = (L.misc & 0xFFFF0000u) | nd | (ns << 8);
@@ -350,69 +346,68 @@ __device__ __forceinline__ void key_event(Lane& L, u32 button, bool pressed) {
 }
 
 __device__ __forceinline__ u32 joy_pull(const Lane& L, u32 v) {
-    u32 p14 = (v >> 4) & 1u, p15 = (v >> 5) & 1u;
+    const u32 p14 = (v >> 4) & 1u, p15 = (v >> 5) & 1u;
     u32 r = (v | 0xCFu) & 0xFFu;
     if (p14 != p15) r &= (!p14) ? bfe8(L.misc, 0) : bfe8(L.misc, 8);
     return r;
 }
 
 // ---------------------------------------------------------------------------------------------
-// memory bus (pyboy mb.getitem / setitem) — oracle: gbcore.c bus_read / bus_write
-__device__ __forceinline__ u32 rom_read(const PkStepArgs& A, const u8* lds_bank0, const Lane& L, u32 a) {
-    if (a < 0x4000u) return lds_bank0[a];
-    u32 bank = bfe8(L.mbc, 0) & A.rom_bank_mask;
-    return A.rom[bank * 0x4000u + (a - 0x4000u)];
-}
-
-__device__ __forceinline__ u32 io_read_special(const Lane& L, u32 a) {
-    switch (a) {
-        case 0xFF04: return bfe8(L.tim0, 0);
-        case 0xFF05: return bfe8(L.tim0, 8);
-        case 0xFF06: return bfe8(L.tim0, 16);
-        case 0xFF07: return bfe8(L.tim0, 24);
-        case 0xFF0F: return G_IF(L);
-        case 0xFF40: return G_LCDC(L);
-        case 0xFF41: return G_STAT(L);
-        case 0xFF42: return bfe8(L.lcd1, 0);
-        case 0xFF43: return bfe8(L.lcd1, 8);
-        case 0xFF44: return G_LY(L);
-        case 0xFF45: return G_LYC(L);
-        case 0xFF46: return 0;
-        case 0xFF47: return bfe8(L.lcd2, 0);
-        case 0xFF48: return bfe8(L.lcd2, 8);
-        case 0xFF49: return bfe8(L.lcd2, 16);
-        case 0xFF4A: return bfe8(L.lcd1, 16);
-        case 0xFF4B: return bfe8(L.lcd1, 24);
-        default: return 0;  // FF10-FF3F: sound not emulated
-    }
-}
-
+// memory bus (pyboy mb.getitem / setitem) — oracle: gbcore.c bus_read / bus_write.
+// Every guest address maps to ONE load: either the ROM (shared, read-only) or the env's
+// lane-interleaved RAM image at phys = addr - off(addr).  Special IO registers live in the lane
+// registers and take a (rare) branch.
 __device__ __forceinline__ bool io_is_special(u32 a) {
-    // FF04-FF07, FF0F, FF10-FF3F (sound), FF40-FF4B
-    return (a >= 0xFF04u && a <= 0xFF07u) || a == 0xFF0Fu || (a >= 0xFF10u && a <= 0xFF4Bu);
+    // FF04-FF07, FF0F, FF10-FF4B (sound: not emulated, LCD), FFFF (IE)
+    return (a >= 0xFF04u && a <= 0xFF07u) || a == 0xFF0Fu || (a >= 0xFF10u && a <= 0xFF4Bu) || a == 0xFFFFu;
 }
 
-__device__ __forceinline__ u32 bus_read(const PkStepArgs& A, const u8* lds_bank0, const Mem& m, const Lane& L, u32 a) {
-    if (a < 0x8000u) return rom_read(A, lds_bank0, L, a);
-    u32 phys;
-    if (a < 0xA000u) {
-        phys = PK_P_VRAM + (a - 0x8000u);
-    } else if (a < 0xC000u) {
-        if (A.mbc == 0u || !bfe8(L.mbc, 16)) return 0xFFu;
-        phys = PK_P_SRAM + (bfe8(L.mbc, 8) & 3u) * 0x2000u + (a - 0xA000u);
-    } else if (a < 0xFE00u) {
-        phys = PK_P_WRAM + (a & 0x1FFFu);
-    } else if (a < 0xFF00u) {
-        phys = PK_P_OAM + (a - 0xFE00u);
-    } else if (a >= 0xFF80u) {
-        if (a == 0xFFFFu) return G_IE(L);
-        phys = PK_P_HRAM + (a - 0xFF80u);
-    } else if (io_is_special(a)) {
-        return io_read_special(L, a);
-    } else {
-        phys = PK_P_IO + (a - 0xFF00u);
+__device__ __noinline__ u32 io_read_special(u32 a, u32 cpu, u32 lcd0, u32 lcd1, u32 lcd2, u32 tim0, u32 divacc) {
+    switch (a) {
+        case 0xFF04: return (divacc >> 8) & 0xFFu;
+        case 0xFF05: return bfe8(tim0, 8);
+        case 0xFF06: return bfe8(tim0, 16);
+        case 0xFF07: return bfe8(tim0, 24);
+        case 0xFF0F: return bfe8(cpu, 16);
+        case 0xFF40: return bfe8(lcd0, 0);
+        case 0xFF41: return bfe8(lcd0, 8);
+        case 0xFF42: return bfe8(lcd1, 0);
+        case 0xFF43: return bfe8(lcd1, 8);
+        case 0xFF44: return bfe8(lcd0, 16);
+        case 0xFF45: return bfe8(lcd0, 24);
+        case 0xFF47: return bfe8(lcd2, 0);
+        case 0xFF48: return bfe8(lcd2, 8);
+        case 0xFF49: return bfe8(lcd2, 16);
+        case 0xFF4A: return bfe8(lcd1, 16);
+        case 0xFF4B: return bfe8(lcd1, 24);
+        case 0xFFFF: return bfe8(cpu, 8);
+        default: return 0;  // FF46 (DMA) and FF10-FF3F (sound not emulated)
     }
-    return ld_phys(m, phys);
+}
+
+// phys offset of a RAM-backed guest address (a >= 0x8000): phys = a - ram_off(a)
+__device__ __forceinline__ u32 ram_off(u32 a, u32 mbcreg) {
+    const u32 sram_off = 0xA000u - PK_P_SRAM - (bfe8(mbcreg, 8) & 3u) * 0x2000u;
+    return a >= 0xFE00u ? 0xBE00u : a >= 0xE000u ? 0xC000u : a >= 0xC000u ? 0xA000u
+         : a >= 0xA000u ? sram_off : 0x8000u;
+}
+
+// ROM bytes staged in LDS (slot 0 = bank 0, then the hottest banks) + the bank -> slot map
+struct RomLds {
+    const u8* bytes;     // nslots * 16 KiB
+    const int8_t* slot;  // [128]
+};
+
+__device__ __forceinline__ u32 bus_read(const PkStepArgs& A, const RomLds& RL, const Mem& m, const Lane& L, u32 a) {
+    const bool rom = a < 0x8000u;
+    const u32 bank = a < 0x4000u ? 0u : (bfe8(L.mbc, 0) & A.rom_bank_mask);
+    const int slot = a < 0x4000u ? 0 : (int)RL.slot[bank & 127u];
+    if (rom && slot >= 0) return RL.bytes[(u32)slot * 0x4000u + (a & 0x3FFFu)];
+    const u8* p = rom ? (A.rom + bank * 0x4000u + (a & 0x3FFFu)) : (m.g + (size_t)((a - ram_off(a, L.mbc)) * PK_LANES + m.lane));
+    u32 v = *p;
+    if ((a & 0xE000u) == 0xA000u && (A.mbc == 0u || !bfe8(L.mbc, 16))) v = 0xFFu;
+    if (io_is_special(a)) v = io_read_special(a, L.cpu, L.lcd0, L.lcd1, L.lcd2, L.tim0, L.divacc);
+    return v;
 }
 
 __device__ __forceinline__ void lcd_set_lcdc(Lane& L, u32 v) {
@@ -420,25 +415,28 @@ __device__ __forceinline__ void lcd_set_lcdc(Lane& L, u32 v) {
     if (!(v & 0x80u)) {
         L.clock = 0;
         L.target = FRAME_CYCLES;
-        (void)stat_set_mode(L, 0u);
+        L.lcd0 = (L.lcd0 & 0xFF0000FFu) | ((G_STAT(L) & 0xFCu) << 8);  // set_mode(0), LY = 0
         L.lcd2 = setb8(L.lcd2, 24, 2u);
-        L.lcd0 = setb8(L.lcd0, 16, 0u);
     }
 }
 
-
-__device__ __forceinline__ void oam_dma(const PkStepArgs& A, const u8* lds_bank0, const Mem& m, Lane& L, u32 env, u32 gid, u32 v) {
-    u32 src = v << 8;
-    FLUSH_PENDING();
-    for (u32 n = 0; n < 0xA0u; n++) {
-        u32 b = bus_read(A, lds_bank0, m, L, (src + n) & 0xFFFFu);
-        st_phys(m, PK_P_OAM + n, b);
+// rare writes: MBC registers, special IO (incl. OAM DMA), IE, joypad select
+__device__ __forceinline__ void bus_write_slow(const PkStepArgs& A, const RomLds& RL, const Mem& m, Lane& L, u32 env, u32 gid, u32 a, u32 v) {
+    if (a < 0x8000u) {  // MBC3.setitem
+        if (A.mbc == 0u) return;
+        if (a < 0x2000u) {
+            L.mbc = setb8(L.mbc, 16, ((v & 0x0Fu) == 0x0Au) ? 1u : 0u);
+        } else if (a < 0x4000u) {
+            v &= 0x7Fu;
+            L.mbc = setb8(L.mbc, 0, v == 0u ? 1u : v);
+        } else if (a < 0x6000u) {
+            L.mbc = setb8(L.mbc, 8, v);
+        }
+        return;
     }
-}
-
-__device__ __forceinline__ void io_write_special(const PkStepArgs& A, const u8* lds_bank0, const Mem& m, Lane& L, u32 env, u32 gid, u32 a, u32 v) {
     switch (a) {
-        case 0xFF04: L.tim0 = setb8(L.tim0, 0, 0u); L.tim1 = 0u; break;
+        case 0xFF00: st_phys(m, PK_P_IO, joy_pull(L, v)); break;
+        case 0xFF04: L.divacc = 0; L.timac = 0; break;
         case 0xFF05: L.tim0 = setb8(L.tim0, 8, v); break;
         case 0xFF06: L.tim0 = setb8(L.tim0, 16, v); break;
         case 0xFF07: L.tim0 = setb8(L.tim0, 24, v & 7u); break;
@@ -447,121 +445,99 @@ __device__ __forceinline__ void io_write_special(const PkStepArgs& A, const u8* 
         case 0xFF41: L.lcd0 = setb8(L.lcd0, 8, (G_STAT(L) & 0x87u) | (v & 0x78u)); break;
         case 0xFF42: L.lcd1 = setb8(L.lcd1, 0, v); break;
         case 0xFF43: L.lcd1 = setb8(L.lcd1, 8, v); break;
-        case 0xFF44: break;
         case 0xFF45: L.lcd0 = setb8(L.lcd0, 24, v); break;
-        case 0xFF46: oam_dma(A, lds_bank0, m, L, env, gid, v); break;
+        case 0xFF46: {  // OAM DMA: instantaneous 160-byte copy (pyboy mb.transfer_DMA)
+            if (L.npend) {
+                flush_lines(A.lat, A.lat_stride, A.screen, m.g, m.lane, env, gid);
+                L.npend = 0;
+            }
+            const u32 src = v << 8;
+            for (u32 n = 0; n < 0xA0u; n++) st_phys(m, PK_P_OAM + n, bus_read(A, RL, m, L, (src + n) & 0xFFFFu));
+            break;
+        }
         case 0xFF47: L.lcd2 = setb8(L.lcd2, 0, v); break;
         case 0xFF48: L.lcd2 = setb8(L.lcd2, 8, v); break;
         case 0xFF49: L.lcd2 = setb8(L.lcd2, 16, v); break;
         case 0xFF4A: L.lcd1 = setb8(L.lcd1, 16, v); break;
         case 0xFF4B: L.lcd1 = setb8(L.lcd1, 24, v); break;
-        default: break;  // sound not emulated
+        case 0xFFFF: S_IE(L, v); break;
+        default: break;  // FF44 (LY, read-only) and FF10-FF3F (sound not emulated)
     }
 }
 
-__device__ __forceinline__ void mbc_write(const PkStepArgs& A, Lane& L, u32 a, u32 v) {
-    if (A.mbc == 0u) return;
-    if (a < 0x2000u) {
-        L.mbc = setb8(L.mbc, 16, ((v & 0x0Fu) == 0x0Au) ? 1u : 0u);
-    } else if (a < 0x4000u) {
-        v &= 0x7Fu;
-        if (v == 0u) v = 1u;
-        L.mbc = setb8(L.mbc, 0, v);
-    } else if (a < 0x6000u) {
-        L.mbc = setb8(L.mbc, 8, v);
-    }
-}
-
-__device__ __forceinline__ void bus_write(const PkStepArgs& A, const u8* lds_bank0, const Mem& m, Lane& L, u32 env, u32 gid, u32 a, u32 v) {
-    if (a < 0x8000u) { mbc_write(A, L, a, v); return; }
-    u32 phys;
-    if (a < 0xA000u) {
-        FLUSH_PENDING();
-        phys = PK_P_VRAM + (a - 0x8000u);
-    } else if (a < 0xC000u) {
-        if (A.mbc == 0u || !bfe8(L.mbc, 16)) return;
-        phys = PK_P_SRAM + (bfe8(L.mbc, 8) & 3u) * 0x2000u + (a - 0xA000u);
-    } else if (a < 0xFE00u) {
-        phys = PK_P_WRAM + (a & 0x1FFFu);
-    } else if (a < 0xFF00u) {
-        if (a < 0xFEA0u) FLUSH_PENDING();
-        phys = PK_P_OAM + (a - 0xFE00u);
-    } else if (a >= 0xFF80u) {
-        if (a == 0xFFFFu) { S_IE(L, v); return; }
-        phys = PK_P_HRAM + (a - 0xFF80u);
-    } else if (a == 0xFF00u) {
-        v = joy_pull(L, v);
-        phys = PK_P_IO;
-    } else if (io_is_special(a)) {
-        io_write_special(A, lds_bank0, m, L, env, gid, a, v);
+__device__ __forceinline__ void bus_write(const PkStepArgs& A, const RomLds& RL, const Mem& m, Lane& L, u32 env, u32 gid, u32 a, u32 v) {
+    if (a < 0x8000u || a == 0xFF00u || io_is_special(a)) {
+        bus_write_slow(A, RL, m, L, env, gid, a, v);
         return;
-    } else {
-        phys = PK_P_IO + (a - 0xFF00u);
     }
-    st_phys(m, phys, v);
+    // VRAM / OAM change while rendered lines are pending: rasterise them first
+    if (L.npend && (a < 0xA000u || (a >= 0xFE00u && a < 0xFEA0u))) {
+        flush_lines(A.lat, A.lat_stride, A.screen, m.g, m.lane, env, gid);
+        L.npend = 0;
+    }
+    if ((a & 0xE000u) == 0xA000u && (A.mbc == 0u || !bfe8(L.mbc, 16))) return;  // SRAM disabled
+    m.g[(size_t)((a - ram_off(a, L.mbc)) * PK_LANES + m.lane)] = (u8)v;
 }
 
 // ---------------------------------------------------------------------------------------------
-// register file helpers (W0 = C|B<<8|E<<16|D<<24, W1 = L|H<<8|A<<16|F<<24)
+// register file helpers (W0 = C|B<<8|E<<16|D<<24, W1 = L|H<<8|A<<16|F<<24).
 // NOTE: selections between lane-state fields are written as arithmetic on VALUES. A C++
 // `cond ? L.w1 : L.w0` (or an if/else storing to one of two fields) lets LLVM form a select of
 // field ADDRESSES, which forces the whole Lane struct into scratch memory.
-__device__ __forceinline__ u32 rd8(const Lane& L, u32 r) {
+__device__ __forceinline__ u32 rd8(u32 w0, u32 w1, u32 r) {
     const u32 sel = 0u - ((r >> 2) & 1u);
-    const u32 w = (L.w0 & ~sel) | (L.w1 & sel);
+    const u32 w = (w0 & ~sel) | (w1 & sel);
     return bfe8(w, ((r ^ 1u) & 3u) * 8u);
 }
-__device__ __forceinline__ void wr8(Lane& L, u32 r, u32 v) {
+// write r8 (r != 6) into (w0, w1)
+__device__ __forceinline__ void wr8(u32& w0, u32& w1, u32 r, u32 v) {
     const u32 sh = ((r ^ 1u) & 3u) * 8u;
     const u32 sel = 0u - ((r >> 2) & 1u);
     const u32 msk = 0xFFu << sh, nv = (v & 0xFFu) << sh;
-    const u32 w0 = L.w0, w1 = L.w1;
-    L.w0 = (w0 & ~(msk & ~sel)) | (nv & ~sel);
-    L.w1 = (w1 & ~(msk & sel)) | (nv & sel);
+    w0 = (w0 & ~(msk & ~sel)) | (nv & ~sel);
+    w1 = (w1 & ~(msk & sel)) | (nv & sel);
 }
-__device__ __forceinline__ u32 rd16(const Lane& L, u32 p) {  // BC DE HL SP
-    const u32 w0 = L.w0, w1 = L.w1, sp = L.sp;
+__device__ __forceinline__ u32 rd16(u32 w0, u32 w1, u32 sp, u32 p) {  // BC DE HL SP
     const u32 lo = (p & 1u) ? (w0 >> 16) : (w0 & 0xFFFFu);
     const u32 hi = (p & 1u) ? sp : (w1 & 0xFFFFu);
     return (p & 2u) ? hi : lo;
 }
-__device__ __forceinline__ void wr16(Lane& L, u32 p, u32 v) {
+__device__ __forceinline__ void wr16(u32& w0, u32& w1, u32& sp, u32 p, u32 v) {
     v &= 0xFFFFu;
-    const u32 w0 = L.w0, w1 = L.w1, sp = L.sp;
     const u32 n0 = p == 0u ? ((w0 & 0xFFFF0000u) | v) : p == 1u ? ((w0 & 0xFFFFu) | (v << 16)) : w0;
     const u32 n1 = p == 2u ? ((w1 & 0xFFFF0000u) | v) : w1;
     const u32 ns = p == 3u ? v : sp;
-    L.w0 = n0;
-    L.w1 = n1;
-    L.sp = ns;
+    w0 = n0;
+    w1 = n1;
+    sp = ns;
 }
-#define A_(L) bfe8((L).w1, 16)
-#define F_(L) bfe8((L).w1, 24)
-#define HL_(L) ((L).w1 & 0xFFFFu)
-#define SETA(L, v) ((L).w1 = setb8((L).w1, 16, (v)))
-#define SETF(L, v) ((L).w1 = setb8((L).w1, 24, (v)))
 
-__device__ __forceinline__ bool cond_ok(const Lane& L, u32 a) {
-    if (!(a & PK_COND_FLAG)) return true;
-    u32 f = F_(L);
-    u32 cc = a & 3u;
-    bool z = (f & 0x80u) != 0, c = (f & 0x10u) != 0;
-    return cc == 0u ? !z : cc == 1u ? z : cc == 2u ? !c : c;
+__device__ __forceinline__ bool cond_ok(u32 f, u32 a) {
+    const u32 cc = a & 3u;
+    const bool z = (f & 0x80u) != 0, c = (f & 0x10u) != 0;
+    const bool t = cc == 0u ? !z : cc == 1u ? z : cc == 2u ? !c : c;
+    return !(a & PK_COND_FLAG) || t;
 }
+
+__device__ __forceinline__ u32 sext8(u32 b) { return (u32)(int)(int8_t)(u8)b; }
 
 // ---------------------------------------------------------------------------------------------
-// K1: the step kernel
+// K1: the step kernel (one lane = one emulator; 24 frames per launch)
 __global__ void __launch_bounds__(256) pk_step_kernel(PkStepArgs A) {
-    __shared__ u8 lds_bank0[0x4000];
-    __shared__ u32 lds_dtab[512];
-    // stage ROM bank 0 (home code + vectors) and the decode table in LDS
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(A.rom);
-        uint4* dst = reinterpret_cast<uint4*>(lds_bank0);
+    __shared__ u32 lds_dtab[1024];
+    __shared__ __attribute__((aligned(16))) u8 lds_rom[PK_LDS_SLOTS * 0x4000u];
+    __shared__ int8_t lds_slot[128];
+    for (u32 i = threadIdx.x; i < 1024u; i += blockDim.x) lds_dtab[i] = A.dtab[i];
+    for (u32 i = threadIdx.x; i < 128u; i += blockDim.x) lds_slot[i] = A.bank_slot[i];
+    for (u32 s = 0; s < A.nslots; s++) {
+        const uint4* src = reinterpret_cast<const uint4*>(A.rom + (size_t)A.slot_bank[s] * 0x4000u);
+        uint4* dst = reinterpret_cast<uint4*>(lds_rom + s * 0x4000u);
         for (u32 i = threadIdx.x; i < 0x4000u / 16u; i += blockDim.x) dst[i] = src[i];
-        for (u32 i = threadIdx.x; i < 512u; i += blockDim.x) lds_dtab[i] = A.dtab[i];
     }
     __syncthreads();
+    RomLds RL;
+    RL.bytes = lds_rom;
+    RL.slot = lds_slot;
 
     const u32 env = blockIdx.x * blockDim.x + threadIdx.x;
     if (env >= A.npad) return;
@@ -584,8 +560,12 @@ __global__ void __launch_bounds__(256) pk_step_kernel(PkStepArgs A) {
     L.lcd0 = R[PK_R_LCD0 * np + env];
     L.lcd1 = R[PK_R_LCD1 * np + env];
     L.lcd2 = R[PK_R_LCD2 * np + env];
-    L.tim0 = R[PK_R_TIM0 * np + env];
-    L.tim1 = R[PK_R_TIM1 * np + env];
+    {
+        const u32 t0 = R[PK_R_TIM0 * np + env], t1 = R[PK_R_TIM1 * np + env];
+        L.tim0 = t0;
+        L.divacc = ((t0 & 0xFFu) << 8) | (t1 & 0xFFu);
+        L.timac = t1 >> 16;
+    }
     L.mbc = R[PK_R_MBC * np + env];
     L.misc = R[PK_R_MISC * np + env];
     L.icount = 0;
@@ -601,296 +581,228 @@ __global__ void __launch_bounds__(256) pk_step_kernel(PkStepArgs A) {
     const u32 btn = action == 0u ? 3u : action == 1u ? 1u : action == 2u ? 0u : action == 3u ? 2u
                   : action == 4u ? 4u : action == 5u ? 5u : action == 6u ? 7u : action == 7u ? 6u : 0xFFu;
     if (active && btn != 0xFFu) key_event(L, btn, true);
-    L.render = (A.render_last && frame + 1u == A.frames) ? 1u : 0u;
     if (active && A.frames > 0u && A.release_frame == 0u && btn != 0xFFu) key_event(L, btn, false);
+    L.render = (A.render_last && frame + 1u == A.frames) ? 1u : 0u;
     if (L.render) {
         u32* lat2 = A.lat + 2u * A.lat_stride;
-        for (u32 y = 0; y < PK_ROWS; y++) {
-            u32 idx = (gid * PK_ROWS + y) * PK_LANES + lane;
-            lat2[idx] &= ~0x100u;
-        }
+        for (u32 y = 0; y < PK_ROWS; y++) lat2[(gid * PK_ROWS + y) * PK_LANES + lane] &= ~0x100u;
     }
 
+    const uint4* rom16 = reinterpret_cast<const uint4*>(A.rom16);
     u32 budget = 0;  // frame watchdog (see oracle/gbcore.c PK_FRAME_BUDGET)
     while (frame < A.frames) {
-        // ---------------- cpu.tick ----------------
-        u32 cycles = 0;
-        u32 d = (PK_C_NOP) | (1u << 6);  // no-op descriptor
-        u32 b1 = 0, b2 = 0;
-        bool exec = false;
-        u32 cpu = L.cpu;
-        u32 intv = 0, intflag = 0;
-        if (cpu & CPU_CRASH) {
-            cycles = 4u;
-        } else {
-            u32 pend = G_IF(L) & G_IE(L) & 0x1Fu;
-            if (!(cpu & CPU_QUEUED) && pend) {
-                if (cpu & CPU_HALT) L.pc = (L.pc + 1u) & 0xFFFFu;
-                if (cpu & CPU_IME) {
-                    intflag = pend & (~pend + 1u);  // lowest set bit = highest priority
-                    intv = 0x40u + 8u * (u32)__builtin_ctz(intflag);
-                    d = PK_C_INT | (PK_M_PUSH2 << 12);
-                }
-                L.cpu = (cpu | CPU_QUEUED) & ~CPU_HALT;
-            } else {
-                if ((cpu & CPU_HALT) && (cpu & CPU_QUEUED)) {
-                    L.cpu = cpu & ~CPU_HALT;
-                    L.pc = (L.pc + 1u) & 0xFFFFu;
-                    exec = true;
-                } else if (cpu & CPU_HALT) {
-                    cycles = 4u;
-                } else {
-                    exec = true;
-                }
-            }
-        }
-        const u32 pc = L.pc;
+        // ---------------- cpu.tick: interrupts / HALT (branch-free) ----------------
+        const u32 cpu = L.cpu;
+        const bool crashed = (cpu & CPU_CRASH) != 0;
+        const bool halted = (cpu & CPU_HALT) != 0;
+        const bool queued = (cpu & CPU_QUEUED) != 0;
+        const u32 pend = G_IF(L) & G_IE(L) & 0x1Fu;
+        const bool do_int = !crashed && !queued && pend != 0u;
+        const bool dispatch = do_int && (cpu & CPU_IME);
+        const bool wake = !crashed && !do_int && halted && queued;
+        const bool exec = !crashed && !do_int && (!halted || queued);
+        const u32 pc = (L.pc + ((do_int && halted) || wake ? 1u : 0u)) & 0xFFFFu;
+        L.cpu = do_int ? ((cpu | CPU_QUEUED) & ~CPU_HALT) : wake ? (cpu & ~CPU_HALT) : cpu;
+        const u32 intflag = pend & (~pend + 1u);  // lowest set bit = highest priority
+        u32 cycles = (crashed || (halted && !exec && !do_int)) ? 4u : 0u;
+
+        // ---------------- fetch + decode: LDS-staged ROM bank, else ONE 16-byte pre-decoded load ----------------
+        u32 d = PK_C_NOP | (1u << 6);
+        u32 u = 0;
+        u32 bytes = 0;
         if (exec) {
-            // fetch: opcode + two operand bytes
-            u32 op;
-            if (pc < 0x3FFEu) {
-                op = lds_bank0[pc]; b1 = lds_bank0[pc + 1u]; b2 = lds_bank0[pc + 2u];
-            } else if (pc >= 0x4000u && pc < 0x7FFEu) {
-                const u8* rb = A.rom + (bfe8(L.mbc, 0) & A.rom_bank_mask) * 0x4000u + (pc - 0x4000u);
-                op = rb[0]; b1 = rb[1]; b2 = rb[2];
-            } else {
-                op = bus_read(A, lds_bank0, m, L, pc);
-                b1 = bus_read(A, lds_bank0, m, L, (pc + 1u) & 0xFFFFu);
-                b2 = bus_read(A, lds_bank0, m, L, (pc + 2u) & 0xFFFFu);
+            const u32 bank = pc < 0x4000u ? 0u : (bfe8(L.mbc, 0) & A.rom_bank_mask);
+            const int slot = pc < 0x4000u ? 0 : (int)lds_slot[bank & 127u];
+            const u32 off = pc & 0x3FFFu;
+            if (pc < 0x8000u && slot >= 0 && off < 0x3FFEu) {
+                // ROM bank staged in LDS: 3 byte reads + decode-table lookup, all LDS
+                const u8* q = lds_rom + (u32)slot * 0x4000u + off;
+                const u32 op = q[0], b1 = q[1], b2 = q[2];
+                const u32 di = op == 0xCBu ? 256u + b1 : op;
+                d = lds_dtab[di];
+                u = lds_dtab[512u + di];
+                bytes = op | (b1 << 8) | (b2 << 16);
+            } else if (pc < 0x8000u && off < 0x3FFEu) {
+                // bank not staged: ONE 16-byte load of the pre-decoded ROM
+                const uint4 e = rom16[bank * 0x4000u + off];
+                d = e.x;
+                u = e.y;
+                bytes = e.z;
+            } else {  // code in RAM / operands across a bank end
+                const u32 op = bus_read(A, RL, m, L, pc);
+                const u32 b1 = bus_read(A, RL, m, L, (pc + 1u) & 0xFFFFu);
+                const u32 b2 = bus_read(A, RL, m, L, (pc + 2u) & 0xFFFFu);
+                const u32 di = op == 0xCBu ? 256u + b1 : op;
+                d = lds_dtab[di];
+                u = lds_dtab[512u + di];
+                bytes = op | (b1 << 8) | (b2 << 16);
             }
-            u32 di = op;
-            if (op == 0xCBu) { di = 256u + b1; }
-            d = lds_dtab[di];
             cycles = PK_D_CYC(d);
             L.icount += 1u;
+            PK_TRACE(env, pc, L.w0, L.w1, L.sp, bytes & 0xFFu);
+        } else if (dispatch) {
+            d = PK_C_INT | (PK_M_PUSH2 << 12);
+            u = (PK_K_INT << 18) | (1u << 22) | (1u << 24);
         }
-        const u32 cls = PK_D_CLS(d);
+        const u32 b1 = bfe8(bytes, 8);
+        const u32 imm16 = (bytes >> 8) & 0xFFFFu;
         const u32 fa = PK_D_A(d), fb = PK_D_B(d), sub = PK_D_OP(d);
-        const u32 hl = HL_(L);
-        const u32 imm16 = b1 | (b2 << 8);
-        const bool taken = cond_ok(L, fa);
+        const u32 ctrl = PK_U_CTRL(u);
+        u32 w0 = L.w0, w1 = L.w1;
+        const u32 sp_old = L.sp;
+        const u32 hl = w1 & 0xFFFFu;
+        u32 f = bfe8(w1, 24);
+        // field a holds a condition only for JP/JR/CALL/RET (RST uses it for the vector)
+        const bool condctl = ctrl == PK_K_JP || ctrl == PK_K_JR || ctrl == PK_K_CALL || ctrl == PK_K_RET;
+        const bool taken = !condctl || cond_ok(f, fa);
 
-        // ---------------- memory reads ----------------
+        // ---------------- memory reads (0, 1 or 2; one load each) ----------------
         u32 rmode = PK_D_RD(d);
-        if (cls == PK_C_RET && !taken) rmode = PK_M_NONE;
+        if (ctrl == PK_K_RET && !taken) rmode = PK_M_NONE;
         u32 m0 = 0, m1 = 0;
         if (rmode != PK_M_NONE) {
-            u32 addr = rmode == PK_M_HL || rmode == PK_M_HLI || rmode == PK_M_HLD ? hl
-                     : rmode == PK_M_BC ? (L.w0 & 0xFFFFu)
-                     : rmode == PK_M_DE ? (L.w0 >> 16)
-                     : rmode == PK_M_NN ? imm16
-                     : rmode == PK_M_HN ? (0xFF00u | b1)
-                     : rmode == PK_M_HC ? (0xFF00u | bfe8(L.w0, 0))
-                     : L.sp;
-            const u32 nr = rmode == PK_M_SP2 ? 2u : 1u;
-            for (u32 k = 0; k < nr; k++) {
-                u32 v = bus_read(A, lds_bank0, m, L, (addr + k) & 0xFFFFu);
-                if (k == 0) m0 = v; else m1 = v;
-            }
+            const u32 addr = (rmode == PK_M_HL || rmode == PK_M_HLI || rmode == PK_M_HLD) ? hl
+                           : rmode == PK_M_BC ? (w0 & 0xFFFFu)
+                           : rmode == PK_M_DE ? (w0 >> 16)
+                           : rmode == PK_M_NN ? imm16
+                           : rmode == PK_M_HN ? (0xFF00u | b1)
+                           : rmode == PK_M_HC ? (0xFF00u | (w0 & 0xFFu))
+                           : sp_old;
+            m0 = bus_read(A, RL, m, L, addr);
+            if (rmode == PK_M_SP2) m1 = bus_read(A, RL, m, L, (addr + 1u) & 0xFFFFu);
         }
 
-        // ---------------- compute ----------------
-        u32 src8 = fb == PK_SRC_IMM ? b1 : fb == 6u ? m0 : rd8(L, fb & 7u);
-        u32 wv0 = 0, wv1 = 0;
+        // ---------------- compute: ONE fused, branch-free datapath driven by the microcode ----------------
+        const u32 a = bfe8(w1, 16);
+        const u32 fc = (f >> 4) & 1u;
+        const u32 tgt = fa == 6u ? m0 : rd8(w0, w1, fa);
+        const u32 src8 = fb == PK_SRC_IMM ? b1 : fb == 6u ? m0 : rd8(w0, w1, fb & 7u);
+        const u32 X = PK_U_XTGT(u) ? tgt : a;
+        const u32 Y = PK_U_YONE(u) ? 1u : src8;
+        // 8-bit adder (ADD ADC SUB SBC CP, INC, DEC)
+        const u32 arith = PK_U_ARITH(u);
+        const bool isSub = arith == 2u || (arith == 0u && (sub == 2u || sub == 3u || sub == 7u));
+        const u32 c_in = (arith == 0u && (sub == 1u || sub == 3u)) ? fc : 0u;
+        const u32 yy = isSub ? (~Y & 0xFFu) : Y;
+        const u32 cin = isSub ? (1u - c_in) : c_in;
+        const u32 r9 = X + yy + cin;
+        const u32 hadd = ((((X & 0xFu) + (yy & 0xFu) + cin) >> 4) & 1u) ^ (isSub ? 1u : 0u);
+        const u32 cadd = ((r9 >> 8) & 1u) ^ (isSub ? 1u : 0u);
+        // logic (AND XOR OR)
+        const u32 lres = sub == 4u ? (X & Y) : sub == 5u ? (X ^ Y) : (X | Y);
+        // rotate/shift unit (RLC RRC RL RR SLA SRA SWAP SRL; RLCA.. use sub-ops 0..3 on A)
+        const u32 rl = ((X << 1) | ((sub & 2u) ? fc : (X >> 7))) & 0xFFu;
+        const u32 rr = (X >> 1) | (((sub & 2u) ? fc : (X & 1u)) << 7);
+        const u32 rot = sub <= 3u ? ((sub & 1u) ? rr : rl)
+                      : sub == 4u ? ((X << 1) & 0xFFu) : sub == 5u ? ((X >> 1) | (X & 0x80u))
+                      : sub == 6u ? (((X >> 4) | (X << 4)) & 0xFFu) : (X >> 1);
+        const u32 rotc = (sub == 0u || sub == 2u || sub == 4u) ? (X >> 7) : sub == 6u ? 0u : (X & 1u);
+        const u32 bm = 1u << (fb & 7u);
+        // DAA (opcodes.py DAA_27) on A
+        u32 corr = ((f & 0x20u) ? 0x06u : 0u) | ((f & 0x10u) ? 0x60u : 0u);
+        corr |= (f & 0x40u) ? 0u : (((a & 0x0Fu) > 0x09u ? 0x06u : 0u) | (a > 0x99u ? 0x60u : 0u));
+        const u32 daa = ((f & 0x40u) ? (a - corr) : (a + corr)) & 0xFFu;
+        const u32 r8sel = PK_U_R8SEL(u);
+        const u32 res8 = r8sel == 1u ? Y : r8sel == 2u ? (r9 & 0xFFu) : r8sel == 3u ? lres : r8sel == 4u ? rot
+                       : r8sel == 5u ? (X & ~bm) : r8sel == 6u ? (X | bm) : r8sel == 7u ? daa : r8sel == 8u ? (~a & 0xFFu) : X;
+        const u32 zf = res8 == 0u ? 0x80u : 0u;
+        // 16-bit unit
+        const u32 op16 = PK_U_OP16(u);
+        const u32 rp = rd16(w0, w1, sp_old, fa);
+        const u32 spe = (sp_old + sext8(b1)) & 0xFFFFu;
+        const u32 popv = m0 | (m1 << 8);
+        const u32 addhl = hl + rp;
+        // flags
+        const u32 fmode = PK_U_FMODE(u);
+        const bool logic = sub >= 4u && sub <= 6u;
+        const u32 f_alu = zf | (isSub ? 0x40u : 0u) | ((logic ? (sub == 4u ? 1u : 0u) : hadd) << 5) | ((logic ? 0u : cadd) << 4);
+        const u32 f_spe = ((((sp_old & 0xFu) + (b1 & 0xFu)) > 0xFu) ? 0x20u : 0u) | ((((sp_old & 0xFFu) + b1) > 0xFFu) ? 0x10u : 0u);
+        f = fmode == PK_F_ALU ? f_alu
+          : fmode == PK_F_INCDEC ? (zf | (isSub ? 0x40u : 0u) | (hadd << 5) | (f & 0x10u))
+          : fmode == PK_F_ROTA ? (rotc << 4)
+          : fmode == PK_F_CBROT ? (zf | (rotc << 4))
+          : fmode == PK_F_BIT ? ((f & 0x10u) | 0x20u | ((X & bm) ? 0u : 0x80u))
+          : fmode == PK_F_DAA ? ((f & 0x40u) | zf | ((corr & 0x60u) ? 0x10u : 0u))
+          : fmode == PK_F_CPL ? (f | 0x60u)
+          : fmode == PK_F_SCF ? ((f & 0x80u) | 0x10u)
+          : fmode == PK_F_CCF ? ((f & 0x80u) | ((f & 0x10u) ^ 0x10u))
+          : fmode == PK_F_ADDHL ? ((f & 0x80u) | ((((hl & 0xFFFu) + (rp & 0xFFFu)) > 0xFFFu) ? 0x20u : 0u) | ((addhl > 0xFFFFu) ? 0x10u : 0u))
+          : fmode == PK_F_ADDSPE ? f_spe
+          : fmode == PK_F_POPAF ? (m0 & 0xF0u)
+          : f;
+        // 8-bit writeback
+        const u32 dst8 = PK_U_DST8(u);
+        if (dst8 == 1u) w1 = setb8(w1, 16, res8);
+        if (dst8 == 2u && fa != 6u) wr8(w0, w1, fa, res8);
+        // 16-bit writeback (pair fa: BC DE HL SP; POP AF special)
+        u32 sp = sp_old;
+        const u32 v16 = op16 == PK_O_LD16 ? imm16 : op16 == PK_O_INC16 ? rp + 1u : op16 == PK_O_DEC16 ? rp - 1u
+                      : op16 == PK_O_POP ? popv : op16 == PK_O_ADDHL ? addhl : spe;
+        const u32 p16 = (op16 == PK_O_ADDHL || op16 == PK_O_SPE_HL) ? 2u : (op16 == PK_O_SPE_SP || op16 == PK_O_SPHL) ? 3u : fa;
+        if (op16 != PK_O_NONE && op16 != PK_O_POPAF) wr16(w0, w1, sp, p16, op16 == PK_O_SPHL ? hl : v16);
+        if (op16 == PK_O_POPAF) w1 = setb8(w1, 16, m1);
+        w1 = setb8(w1, 24, f);
+        // control transfer
         u32 npc = (pc + PK_D_LEN(d)) & 0xFFFFu;
-        u32 nsp = L.sp;
-        u32 f = F_(L);
-        switch (cls) {
-            case PK_C_NOP: break;
-            case PK_C_LD8:
-                if (fa != 6u) wr8(L, fa, src8);
-                wv0 = src8;
-                break;
-            case PK_C_ALU: {
-                u32 a = A_(L), v = src8, c = (f >> 4) & 1u, r = 0;
-                switch (sub) {
-                    case 0: r = a + v; f = (((r & 0xFFu) == 0) ? 0x80u : 0) | ((((a & 0xFu) + (v & 0xFu)) > 0xFu) ? 0x20u : 0) | ((r > 0xFFu) ? 0x10u : 0); break;
-                    case 1: r = a + v + c; f = (((r & 0xFFu) == 0) ? 0x80u : 0) | ((((a & 0xFu) + (v & 0xFu) + c) > 0xFu) ? 0x20u : 0) | ((r > 0xFFu) ? 0x10u : 0); break;
-                    case 2:
-                    case 7: r = a - v; f = 0x40u | (((r & 0xFFu) == 0) ? 0x80u : 0) | (((a & 0xFu) < (v & 0xFu)) ? 0x20u : 0) | ((a < v) ? 0x10u : 0); if (sub == 7u) r = a; break;
-                    case 3: r = a - v - c; f = 0x40u | (((r & 0xFFu) == 0) ? 0x80u : 0) | (((a & 0xFu) < (v & 0xFu) + c) ? 0x20u : 0) | ((a < v + c) ? 0x10u : 0); break;
-                    case 4: r = a & v; f = ((r == 0) ? 0x80u : 0) | 0x20u; break;
-                    case 5: r = a ^ v; f = (r == 0) ? 0x80u : 0; break;
-                    default: r = a | v; f = (r == 0) ? 0x80u : 0; break;
-                }
-                SETA(L, r & 0xFFu);
-                break;
-            }
-            case PK_C_INC8: {
-                u32 v = fa == 6u ? m0 : rd8(L, fa), r = (v + 1u) & 0xFFu;
-                f = (f & 0x10u) | (r == 0 ? 0x80u : 0) | (((v & 0xFu) == 0xFu) ? 0x20u : 0);
-                if (fa != 6u) wr8(L, fa, r);
-                wv0 = r;
-                break;
-            }
-            case PK_C_DEC8: {
-                u32 v = fa == 6u ? m0 : rd8(L, fa), r = (v - 1u) & 0xFFu;
-                f = (f & 0x10u) | 0x40u | (r == 0 ? 0x80u : 0) | (((v & 0xFu) == 0u) ? 0x20u : 0);
-                if (fa != 6u) wr8(L, fa, r);
-                wv0 = r;
-                break;
-            }
-            case PK_C_ROTA:
-            case PK_C_CBROT: {
-                u32 v = cls == PK_C_ROTA ? A_(L) : (fa == 6u ? m0 : rd8(L, fa));
-                u32 c, r;
-                u32 fc = (f >> 4) & 1u;
-                switch (sub) {
-                    case 0: c = v >> 7; r = (v << 1) | c; break;
-                    case 1: c = v & 1u; r = (v >> 1) | (c << 7); break;
-                    case 2: c = v >> 7; r = (v << 1) | fc; break;
-                    case 3: c = v & 1u; r = (v >> 1) | (fc << 7); break;
-                    case 4: c = v >> 7; r = v << 1; break;
-                    case 5: c = v & 1u; r = (v >> 1) | (v & 0x80u); break;
-                    case 6: c = 0; r = (v >> 4) | (v << 4); break;
-                    default: c = v & 1u; r = v >> 1; break;
-                }
-                r &= 0xFFu;
-                if (cls == PK_C_ROTA) {
-                    f = c ? 0x10u : 0u;
-                    SETA(L, r);
-                } else {
-                    f = (r == 0 ? 0x80u : 0) | (c ? 0x10u : 0u);
-                    if (fa != 6u) wr8(L, fa, r);
-                    wv0 = r;
-                }
-                break;
-            }
-            case PK_C_BIT: {
-                u32 v = fa == 6u ? m0 : rd8(L, fa);
-                f = (f & 0x10u) | 0x20u | ((v & (1u << fb)) ? 0u : 0x80u);
-                break;
-            }
-            case PK_C_RES:
-            case PK_C_SET: {
-                u32 v = fa == 6u ? m0 : rd8(L, fa);
-                u32 r = cls == PK_C_RES ? (v & ~(1u << fb)) : (v | (1u << fb));
-                if (fa != 6u) wr8(L, fa, r);
-                wv0 = r & 0xFFu;
-                break;
-            }
-            case PK_C_LD16: wr16(L, fa, imm16); nsp = L.sp; break;
-            case PK_C_INC16: wr16(L, fa, rd16(L, fa) + 1u); nsp = L.sp; break;
-            case PK_C_DEC16: wr16(L, fa, rd16(L, fa) - 1u); nsp = L.sp; break;
-            case PK_C_ADDHL: {
-                u32 v = rd16(L, fa), r = hl + v;
-                f = (f & 0x80u) | ((((hl & 0xFFFu) + (v & 0xFFFu)) > 0xFFFu) ? 0x20u : 0) | ((r > 0xFFFFu) ? 0x10u : 0);
-                L.w1 = (L.w1 & 0xFFFF0000u) | (r & 0xFFFFu);
-                break;
-            }
-            case PK_C_ADDSP:
-            case PK_C_LDHLSP: {
-                u32 sp = L.sp;
-                u32 r = (sp + (u32)(int)(int8_t)(u8)b1) & 0xFFFFu;
-                f = ((((sp & 0xFu) + (b1 & 0xFu)) > 0xFu) ? 0x20u : 0) | ((((sp & 0xFFu) + b1) > 0xFFu) ? 0x10u : 0);
-                if (cls == PK_C_ADDSP) nsp = r;
-                else L.w1 = (L.w1 & 0xFFFF0000u) | r;
-                break;
-            }
-            case PK_C_LDSPHL: nsp = hl; break;
-            case PK_C_LDNNSP: wv0 = L.sp & 0xFFu; wv1 = L.sp >> 8; break;
-            case PK_C_JP: if (taken) { npc = imm16; cycles += PK_D_XCYC(d); } break;
-            case PK_C_JPHL: npc = hl; break;
-            case PK_C_JR: if (taken) { npc = (pc + 2u + (u32)(int)(int8_t)(u8)b1) & 0xFFFFu; cycles += PK_D_XCYC(d); } break;
-            case PK_C_CALL:
-                if (taken) {
-                    wv0 = npc >> 8; wv1 = npc & 0xFFu;
-                    nsp = (L.sp - 2u) & 0xFFFFu;
-                    npc = imm16;
-                    cycles += PK_D_XCYC(d);
-                }
-                break;
-            case PK_C_RET:
-            case PK_C_RETI:
-                if (taken) {
-                    npc = m0 | (m1 << 8);
-                    nsp = (L.sp + 2u) & 0xFFFFu;
-                    cycles += PK_D_XCYC(d);
-                    if (cls == PK_C_RETI) L.cpu |= CPU_IME;
-                }
-                break;
-            case PK_C_RST:
-                wv0 = npc >> 8; wv1 = npc & 0xFFu;
-                nsp = (L.sp - 2u) & 0xFFFFu;
-                npc = fa * 8u;
-                break;
-            case PK_C_PUSH: {
-                u32 v = fa == 3u ? ((A_(L) << 8) | f) : rd16(L, fa);
-                wv0 = v >> 8; wv1 = v & 0xFFu;
-                nsp = (L.sp - 2u) & 0xFFFFu;
-                break;
-            }
-            case PK_C_POP: {
-                u32 v = m0 | (m1 << 8);
-                if (fa == 3u) { SETA(L, v >> 8); f = v & 0xF0u; }
-                else wr16(L, fa, v);
-                nsp = (L.sp + 2u) & 0xFFFFu;
-                break;
-            }
-            case PK_C_DAA: {
-                int t = (int)A_(L);
-                u32 corr = 0;
-                if (f & 0x20u) corr |= 0x06u;
-                if (f & 0x10u) corr |= 0x60u;
-                if (f & 0x40u) t -= (int)corr;
-                else {
-                    if ((t & 0x0F) > 0x09) corr |= 0x06u;
-                    if (t > 0x99) corr |= 0x60u;
-                    t += (int)corr;
-                }
-                f = (f & 0x40u) | (((t & 0xFF) == 0) ? 0x80u : 0) | ((corr & 0x60u) ? 0x10u : 0);
-                SETA(L, (u32)t & 0xFFu);
-                break;
-            }
-            case PK_C_CPL: SETA(L, (~A_(L)) & 0xFFu); f |= 0x60u; break;
-            case PK_C_SCF: f = (f & 0x80u) | 0x10u; break;
-            case PK_C_CCF: f = (f & 0x80u) | ((f & 0x10u) ^ 0x10u); break;
-            case PK_C_DI: L.cpu &= ~CPU_IME; break;
-            case PK_C_EI: L.cpu |= CPU_IME; break;
-            case PK_C_HALT: L.cpu |= CPU_HALT; npc = pc; break;
-            case PK_C_ILLEGAL: L.cpu |= CPU_CRASH | CPU_HALT; npc = pc; break;
-            case PK_C_INT:
-                wv0 = pc >> 8; wv1 = pc & 0xFFu;
-                nsp = (L.sp - 2u) & 0xFFFFu;
-                npc = intv;
-                S_IF(L, G_IF(L) ^ intflag);
-                L.cpu &= ~CPU_IME;
-                break;
-            default: break;
-        }
-        SETF(L, f);
-
-        // ---------------- memory writes ----------------
+        const u32 push_pc = ctrl == PK_K_INT ? pc : npc;
+        const u32 jr_t = (pc + 2u + sext8(b1)) & 0xFFFFu;
+        const u32 tgt_pc = ctrl == PK_K_JP || ctrl == PK_K_CALL ? imm16 : ctrl == PK_K_JPHL ? hl : ctrl == PK_K_JR ? jr_t
+                         : (ctrl == PK_K_RET || ctrl == PK_K_RETI) ? popv : ctrl == PK_K_RST ? fa * 8u
+                         : ctrl == PK_K_INT ? 0x40u + 8u * (u32)__builtin_ctz(intflag | 0x20u) : pc;
+        const bool jump = ctrl != PK_K_SEQ && taken;
+        npc = jump ? tgt_pc : npc;
+        if (jump && ctrl <= PK_K_RETI) cycles += PK_D_XCYC(d);
+        u32 cpu2 = L.cpu;
+        const u32 ime = PK_U_IME(u);
+        cpu2 = ime == 1u ? (cpu2 & ~CPU_IME) : ime == 2u ? (cpu2 | CPU_IME) : cpu2;
+        cpu2 |= ctrl == PK_K_HALT ? CPU_HALT : ctrl == PK_K_ILLEGAL ? (CPU_CRASH | CPU_HALT) : 0u;
+        if (ctrl == PK_K_INT) cpu2 ^= intflag << 16;   // IF ^= flag
+        L.cpu = cpu2;
+        // write data
+        const u32 wsrc = PK_U_WSRC(u);
+        const u32 pushv = wsrc == 1u ? push_pc : (fa == 3u ? ((a << 8) | bfe8(L.w1, 24)) : rp);
+        const u32 wv0 = wsrc == 0u ? res8 : wsrc == 3u ? (sp_old & 0xFFu) : (pushv >> 8);
+        const u32 wv1 = wsrc == 3u ? (sp_old >> 8) : (pushv & 0xFFu);
         u32 wmode = PK_D_WR(d);
-        if (cls == PK_C_CALL && !taken) wmode = PK_M_NONE;
+        if (ctrl == PK_K_CALL && !taken) wmode = PK_M_NONE;
+        // stack pointer moves of PUSH/CALL/RST/INT (PUSH2) and POP/RET (SP2)
+        if (wmode == PK_M_PUSH2) sp = (sp_old - 2u) & 0xFFFFu;
+        if (rmode == PK_M_SP2) sp = (sp_old + 2u) & 0xFFFFu;
+
+        // ---------------- memory writes (0, 1 or 2; one store each) ----------------
+        L.w0 = w0;
+        L.w1 = w1;
         if (wmode != PK_M_NONE) {
-            u32 addr = wmode == PK_M_HL || wmode == PK_M_HLI || wmode == PK_M_HLD ? hl
-                     : wmode == PK_M_BC ? (L.w0 & 0xFFFFu)
-                     : wmode == PK_M_DE ? (L.w0 >> 16)
-                     : wmode == PK_M_NN || wmode == PK_M_NN2 ? imm16
-                     : wmode == PK_M_HN ? (0xFF00u | b1)
-                     : wmode == PK_M_HC ? (0xFF00u | bfe8(L.w0, 0))
-                     : ((L.sp - 1u) & 0xFFFFu);
+            const u32 addr = (wmode == PK_M_HL || wmode == PK_M_HLI || wmode == PK_M_HLD) ? hl
+                           : wmode == PK_M_BC ? (w0 & 0xFFFFu)
+                           : wmode == PK_M_DE ? (w0 >> 16)
+                           : (wmode == PK_M_NN || wmode == PK_M_NN2) ? imm16
+                           : wmode == PK_M_HN ? (0xFF00u | b1)
+                           : wmode == PK_M_HC ? (0xFF00u | (w0 & 0xFFu))
+                           : ((sp_old - 1u) & 0xFFFFu);
             const u32 nw = (wmode == PK_M_PUSH2 || wmode == PK_M_NN2) ? 2u : 1u;
+#pragma unroll 1
             for (u32 k = 0; k < nw; k++) {
-                u32 wa = wmode == PK_M_PUSH2 ? ((addr - k) & 0xFFFFu) : ((addr + k) & 0xFFFFu);
-                bus_write(A, lds_bank0, m, L, env, gid, wa, k == 0 ? wv0 : wv1);
+                const u32 wa = k == 0u ? addr : wmode == PK_M_PUSH2 ? ((addr - 1u) & 0xFFFFu) : ((addr + 1u) & 0xFFFFu);
+                bus_write(A, RL, m, L, env, gid, wa, k == 0u ? wv0 : wv1);
             }
         }
         // HL post-increment/decrement ((HL+)/(HL-) forms)
         if (rmode == PK_M_HLI || wmode == PK_M_HLI) L.w1 = (L.w1 & 0xFFFF0000u) | ((hl + 1u) & 0xFFFFu);
         if (rmode == PK_M_HLD || wmode == PK_M_HLD) L.w1 = (L.w1 & 0xFFFF0000u) | ((hl - 1u) & 0xFFFFu);
-        if (exec || cls == PK_C_INT) {
+        if (exec || dispatch) {
             L.pc = npc;
-            L.sp = nsp;
+            L.sp = sp;
+        } else {
+            L.pc = pc;
         }
         if (exec) L.cpu &= ~CPU_QUEUED;
 
         // ---------------- HALT fast-forward + timer + LCD (pyboy mb.tick) ----------------
         if (L.cpu & CPU_HALT) {
-            int a = (int)L.target - (int)L.clock;
-            int b = timer_cycles_to_interrupt(L);
-            int mm = a < b ? a : b;
+            const int ta = (int)L.target - (int)L.clock;
+            const int tb = timer_cycles_to_interrupt(L);
+            const int mm = ta < tb ? ta : tb;
             cycles = mm < 0 ? 0u : (u32)mm;
         }
         u32 irq = timer_tick(L, cycles);
@@ -906,10 +818,7 @@ __global__ void __launch_bounds__(256) pk_step_kernel(PkStepArgs A) {
             L.render = (A.render_last && frame + 1u == A.frames) ? 1u : 0u;
             if (L.render) {
                 u32* lat2 = A.lat + 2u * A.lat_stride;
-                for (u32 y = 0; y < PK_ROWS; y++) {
-                    u32 idx = (gid * PK_ROWS + y) * PK_LANES + lane;
-                    lat2[idx] &= ~0x100u;
-                }
+                for (u32 y = 0; y < PK_ROWS; y++) lat2[(gid * PK_ROWS + y) * PK_LANES + lane] &= ~0x100u;
             }
         }
     }
@@ -925,8 +834,8 @@ __global__ void __launch_bounds__(256) pk_step_kernel(PkStepArgs A) {
     R[PK_R_LCD0 * np + env] = L.lcd0;
     R[PK_R_LCD1 * np + env] = L.lcd1;
     R[PK_R_LCD2 * np + env] = L.lcd2;
-    R[PK_R_TIM0 * np + env] = L.tim0;
-    R[PK_R_TIM1 * np + env] = L.tim1;
+    R[PK_R_TIM0 * np + env] = (L.tim0 & 0xFFFFFF00u) | ((L.divacc >> 8) & 0xFFu);
+    R[PK_R_TIM1 * np + env] = (L.divacc & 0xFFu) | (L.timac << 16);
     R[PK_R_MBC * np + env] = L.mbc;
     R[PK_R_MISC * np + env] = L.misc;
     R[PK_R_TIME * np + env] += 1u;

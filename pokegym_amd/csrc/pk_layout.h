@@ -22,6 +22,9 @@
 #pragma once
 #include <stdint.h>
 
+typedef struct { uint32_t x, y; } uint2_t;
+typedef struct { uint32_t desc, ucode, bytes, pad; } pk_rom_entry;  // 16-byte pre-decoded ROM entry
+
 #define PK_LANES 64u
 #define PK_PHYS 0xC200u
 #define PK_GROUP_STRIDE (PK_PHYS * PK_LANES)
@@ -80,15 +83,41 @@ enum {  // memory addressing modes (read and write)
     PK_M_NN2     // write: [nn]=lo, [nn+1]=hi    (LD (nn),SP)
 };
 
-enum {  // datapath classes
-    PK_C_NOP = 0, PK_C_LD8, PK_C_ALU, PK_C_INC8, PK_C_DEC8, PK_C_ROTA, PK_C_CBROT, PK_C_BIT,
-    PK_C_RES, PK_C_SET, PK_C_LD16, PK_C_INC16, PK_C_DEC16, PK_C_ADDHL, PK_C_ADDSP, PK_C_LDHLSP,
-    PK_C_LDSPHL, PK_C_LDNNSP, PK_C_JP, PK_C_JPHL, PK_C_JR, PK_C_CALL, PK_C_RET, PK_C_RETI,
-    PK_C_RST, PK_C_PUSH, PK_C_POP, PK_C_DAA, PK_C_CPL, PK_C_SCF, PK_C_CCF, PK_C_DI, PK_C_EI,
-    PK_C_HALT, PK_C_ILLEGAL, PK_C_INT, PK_C_COUNT
+// datapath classes: class = family << 3 | index, so the kernel dispatches on 6 families and
+// computes the classes inside a family with selects (no per-opcode branches).
+enum {
+    PK_C_LD8 = 0x00,                                                     // family 0: loads
+    PK_C_ALU = 0x08, PK_C_INC8, PK_C_DEC8,                               // family 1: 8-bit arithmetic
+    PK_C_ROTA = 0x10, PK_C_CBROT, PK_C_BIT, PK_C_RES, PK_C_SET, PK_C_DAA, PK_C_CPL,
+    PK_C_SCFCCF,                                                         // family 2: bit/rotate/misc 8-bit
+    PK_C_LD16 = 0x18, PK_C_INCDEC16, PK_C_ADDHL, PK_C_ADDSPE, PK_C_LDSPHL, PK_C_LDNNSP, PK_C_PUSH,
+    PK_C_POP,                                                            // family 3: 16-bit
+    PK_C_JP = 0x20, PK_C_JPHL, PK_C_JR, PK_C_CALL, PK_C_RET, PK_C_RETI, PK_C_RST,
+    PK_C_INT,                                                            // family 4: control flow
+    PK_C_NOP = 0x28, PK_C_DI, PK_C_EI, PK_C_HALT, PK_C_ILLEGAL           // family 5: misc
 };
+#define PK_FAMILY(cls) ((cls) >> 3)
 
-#define PK_SRC_IMM 8u  // field b of LD8/ALU: source is the immediate byte
+// second descriptor word: microcode controlling the fused (branch-free) datapath
+#define PK_U_R8SEL(u) ((u) & 15u)           // result8: 0 keep 1 Y 2 ADD 3 LOGIC 4 ROT 5 RES 6 SET 7 DAA 8 CPL
+#define PK_U_DST8(u) (((u) >> 4) & 3u)      // 0 none, 1 A, 2 r[fa] (mem if fa==6)
+#define PK_U_XTGT(u) (((u) >> 6) & 1u)      // X = tgt (r[fa]/m0) instead of A
+#define PK_U_YONE(u) (((u) >> 7) & 1u)      // Y = 1 (INC/DEC)
+#define PK_U_ARITH(u) (((u) >> 8) & 3u)     // adder: 0 from ALU sub-op, 1 INC, 2 DEC
+#define PK_U_FMODE(u) (((u) >> 10) & 15u)   // flags: see PK_F_*
+#define PK_U_OP16(u) (((u) >> 14) & 15u)    // 16-bit op: see PK_O_*
+#define PK_U_CTRL(u) (((u) >> 18) & 15u)    // control: see PK_K_*
+#define PK_U_WSRC(u) (((u) >> 22) & 3u)     // write data: 0 res8, 1 push PC, 2 push pair, 3 SP lo/hi
+#define PK_U_IME(u) (((u) >> 24) & 3u)      // 0 keep, 1 clear, 2 set
+enum { PK_F_KEEP = 0, PK_F_ALU, PK_F_INCDEC, PK_F_ROTA, PK_F_CBROT, PK_F_BIT, PK_F_DAA, PK_F_CPL, PK_F_SCF,
+       PK_F_CCF, PK_F_ADDHL, PK_F_ADDSPE, PK_F_POPAF };
+enum { PK_O_NONE = 0, PK_O_LD16, PK_O_INC16, PK_O_DEC16, PK_O_ADDHL, PK_O_SPE_SP, PK_O_SPE_HL, PK_O_SPHL,
+       PK_O_POP, PK_O_POPAF };
+enum { PK_K_SEQ = 0, PK_K_JP, PK_K_JPHL, PK_K_JR, PK_K_CALL, PK_K_RET, PK_K_RETI, PK_K_RST, PK_K_INT,
+       PK_K_HALT, PK_K_ILLEGAL };
+
+#define PK_SRC_IMM 8u
+#define PK_LDS_SLOTS 6u  // ROM banks (16 KiB each) staged in LDS by the step kernel  // field b of LD8/ALU: source is the immediate byte
 #define PK_COND_ALWAYS 0u
 #define PK_COND_FLAG 4u  // field a bit 2 set: conditional; bits 0..1 = nz,z,nc,c
 
@@ -96,8 +125,9 @@ enum {  // datapath classes
 struct PkStepArgs {
     uint8_t* mem;             // lane-interleaved RAM images
     const uint8_t* rom;       // whole ROM
+    const pk_rom_entry* rom16; // pre-decoded ROM: per ROM byte {desc, ucode, op|b1<<8|b2<<16|slow<<24, 0}
     uint32_t* regs;           // SoA lane registers [PK_NREGS][npad]
-    const uint32_t* dtab;     // 512 decode descriptors
+    const uint32_t* dtab;     // 512 decode descriptors + 512 microcode words
     const uint8_t* actions;   // [n] action ids (0..7; >=8 = no button)
     uint32_t* lat;            // [3][ngroups*144*64] per-line render latches
     uint8_t* screen;          // [n][144][160] persistent grey screen
@@ -108,6 +138,9 @@ struct PkStepArgs {
     uint32_t release_frame;   // 8
     uint32_t render_last;     // rasterise the last frame
     uint32_t lat_stride;      // ngroups*144*64
+    uint32_t nslots;          // ROM banks staged in LDS (slot 0 = bank 0)
+    const int8_t* bank_slot;  // [128] LDS slot of each ROM bank, -1 = not staged
+    const uint8_t* slot_bank; // [PK_LDS_SLOTS] bank held by each slot
 };
 
 struct PkResetArgs {

@@ -1,0 +1,73 @@
+// Host-simulation shim for the HIP runtime — TEST INFRASTRUCTURE ONLY.
+//
+// Lets tests compile the unmodified kernels (pokegym_amd/csrc/pk_kernels.hip) and C ABI
+// (pk_capi.cpp) with g++ and run them on the CPU: every workgroup runs as blockDim OS threads
+// joined by a std::barrier at __syncthreads(); __shared__ arrays are per-block statics (one block
+// runs at a time).  Device memory is host memory.  This checks kernel LOGIC against the oracle
+// without a GPU; the real gfx950 build is what ships and is checked by the -m gpu tests.
+#pragma once
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <barrier>
+#include <functional>
+#include <thread>
+#include <vector>
+
+#define __global__
+#define __device__
+#define __host__
+#define __shared__ static
+#define __constant__ static const
+#define __forceinline__ inline __attribute__((always_inline))
+#define __noinline__ __attribute__((noinline))
+#define __launch_bounds__(...)
+#define __builtin_amdgcn_readfirstlane(x) (x)
+
+struct dim3 {
+    unsigned x, y, z;
+    dim3(unsigned a = 1, unsigned b = 1, unsigned c = 1) : x(a), y(b), z(c) {}
+};
+struct uint2 { uint32_t x, y; };
+struct uint4 { uint32_t x, y, z, w; };
+static inline uint2 make_uint2(uint32_t a, uint32_t b) { return uint2{a, b}; }
+static inline uint4 make_uint4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return uint4{a, b, c, d}; }
+
+extern thread_local dim3 threadIdx;
+extern thread_local dim3 blockIdx;
+extern dim3 blockDim;
+extern dim3 gridDim;
+extern std::barrier<>* pk_sim_barrier;
+static inline void __syncthreads() { pk_sim_barrier->arrive_and_wait(); }
+
+typedef int hipError_t;
+typedef void* hipStream_t;
+typedef void* hipEvent_t;
+enum { hipSuccess = 0, hipErrorOutOfMemory = 2 };
+enum hipMemcpyKind { hipMemcpyHostToDevice, hipMemcpyDeviceToHost, hipMemcpyDeviceToDevice, hipMemcpyHostToHost };
+static inline const char* hipGetErrorString(hipError_t) { return "hostsim error"; }
+static inline hipError_t hipGetLastError() { return hipSuccess; }
+static inline hipError_t hipSetDevice(int) { return hipSuccess; }
+static inline hipError_t hipDeviceSynchronize() { return hipSuccess; }
+static inline hipError_t hipMalloc(void** p, size_t n) {
+    *p = aligned_alloc(256, (n + 255) / 256 * 256);
+    return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+static inline hipError_t hipFree(void* p) { free(p); return hipSuccess; }
+static inline hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind) { memmove(d, s, n); return hipSuccess; }
+static inline hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipStream_t) { memmove(d, s, n); return hipSuccess; }
+static inline hipError_t hipMemset(void* d, int v, size_t n) { memset(d, v, n); return hipSuccess; }
+static inline hipError_t hipEventCreate(hipEvent_t* e) { *e = nullptr; return hipSuccess; }
+static inline hipError_t hipEventDestroy(hipEvent_t) { return hipSuccess; }
+static inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
+static inline hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
+static inline hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) { *ms = 0.f; return hipSuccess; }
+
+void pk_sim_launch(dim3 grid, dim3 block, const std::function<void()>& body);
+#define hipLaunchKernelGGL(k, grid, block, shmem, stream, ...) \
+    pk_sim_launch(dim3(grid), dim3(block), [&]() { k(__VA_ARGS__); })
+
+// instruction trace for debugging (env, pc, w0, w1, sp, opcode)
+extern "C" void pk_sim_trace(uint32_t env, uint32_t pc, uint32_t w0, uint32_t w1, uint32_t sp, uint32_t op);
+#define PK_TRACE(env, pc, w0, w1, sp, op) pk_sim_trace(env, pc, w0, w1, sp, op)

@@ -1,0 +1,55 @@
+// Host-simulation runtime (see hip/hip_runtime.h). TEST INFRASTRUCTURE ONLY.
+#include "hip/hip_runtime.h"
+
+thread_local dim3 threadIdx;
+thread_local dim3 blockIdx;
+dim3 blockDim;
+dim3 gridDim;
+std::barrier<>* pk_sim_barrier = nullptr;
+
+void pk_sim_launch(dim3 grid, dim3 block, const std::function<void()>& body) {
+    // blockDim.x OS threads walk the blocks in order; a barrier at the end of every block keeps
+    // the per-block __shared__ statics private to the block being run.
+    gridDim = grid;
+    blockDim = block;
+    std::barrier<> bar((ptrdiff_t)block.x);
+    pk_sim_barrier = &bar;
+    std::vector<std::thread> ts;
+    ts.reserve(block.x);
+    for (unsigned t = 0; t < block.x; t++)
+        ts.emplace_back([&, t]() {
+            for (unsigned b = 0; b < grid.x; b++) {
+                blockIdx = dim3(b);
+                threadIdx = dim3(t);
+                body();
+                bar.arrive_and_wait();
+            }
+        });
+    for (auto& th : ts) th.join();
+}
+
+#include <mutex>
+static std::vector<uint32_t> g_trace;
+static uint32_t g_trace_env = 0xFFFFFFFFu;
+static size_t g_trace_cap = 0;
+static std::mutex g_trace_mu;
+extern "C" void pk_sim_trace_enable(uint32_t env, uint64_t cap) {
+    std::lock_guard<std::mutex> l(g_trace_mu);
+    g_trace.clear();
+    g_trace_env = env;
+    g_trace_cap = cap;
+}
+extern "C" void pk_sim_trace(uint32_t env, uint32_t pc, uint32_t w0, uint32_t w1, uint32_t sp, uint32_t op) {
+    if (env != g_trace_env) return;
+    std::lock_guard<std::mutex> l(g_trace_mu);
+    if (g_trace.size() / 6 >= g_trace_cap) return;
+    uint32_t rec[6] = {pc, w0, w1, sp, op, 0};
+    g_trace.insert(g_trace.end(), rec, rec + 6);
+}
+extern "C" uint64_t pk_sim_trace_get(uint32_t* out, uint64_t cap) {
+    std::lock_guard<std::mutex> l(g_trace_mu);
+    uint64_t n = g_trace.size() / 6;
+    if (n > cap) n = cap;
+    memcpy(out, g_trace.data(), n * 6 * 4);
+    return n;
+}
