@@ -26,6 +26,7 @@ sys.path.insert(0, HERE)
 S_HOT = 8192 + 8192 + 160 + 127 + 128 + 1 + 44
 B_HEADLESS = 2 * S_HOT + 1 + 8 + 2          # 33,699: K1 reads+writes the hot state, action, reward, flags
 B_SCREEN = B_HEADLESS + 160 * 144           # 56,739: + the u8 screen obs (K2)
+B_REWARD = B_SCREEN + 2 * 256               # 57,251: + per-env reward accumulators (config 5)
 HBM_PEAK_GBS = 8000.0                       # MI355X_MICROARCH.md: 8.0 TB/s HBM3E
 
 
@@ -65,8 +66,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
-    ap.add_argument("--workload", choices=["config3", "config2"], default="config3",
-                    help="config3: rendered screen obs + random actions; config2: headless, fixed action cycle")
+    ap.add_argument("--workload", choices=["config3", "config2", "config5"], default="config3",
+                    help="config3: rendered screen obs + random actions; config2: headless, fixed action cycle; "
+                         "config5: config3 + reward stack + (72,80,4) obs + per-env reset on done + stats all-reduce")
     ap.add_argument("--actions", choices=["auto", "random", "same"], default="auto",
                     help="override the workload's action stream (diagnostics)")
     ap.add_argument("--rom", default=None)
@@ -96,15 +98,35 @@ def main():
         rom_name = "pkbench (synthetic game ROM; pokemon_red.gb is not shipped)"
     state = open(args.state, "rb").read() if args.state else None
 
-    render = args.workload == "config3"
+    render = args.workload in ("config3", "config5")
+    reward = args.workload == "config5"
     n = args.envs
-    emu = BatchedEmulator(rom, n, state=state, device=local, render=render)
+    emu = BatchedEmulator(rom, n, state=state, device=local, render=render, reward=reward,
+                          reload_on_reset=reward)
+    if reward:
+        emu.reset()
+    ep_ret = torch.zeros(n, dtype=torch.float64, device=dev)
+    stats = torch.zeros(2, dtype=torch.float64, device=dev)  # [sum of episodic returns, episodes]
+
+    def env_step(t):
+        obs, rew, term, trunc = emu.step(acts[t])
+        if reward:
+            # per-env reload of the template state on done, episodic-return bookkeeping, and the
+            # RCCL all-reduce of the episode statistics every 128 steps (configs[4])
+            d = term.to(torch.float64)
+            ep_ret.add_(rew)
+            stats[0] += (ep_ret * d).sum()
+            stats[1] += d.sum()
+            ep_ret.mul_(1.0 - d)
+            emu.reset(term)
+            if world > 1 and t % 128 == 127:
+                dist.all_reduce(stats)
     total = args.warmup + args.steps
     if args.actions == "same":
         g = torch.Generator(device=dev)
         g.manual_seed(1234 + rank)
         acts = torch.randint(0, 8, (total, 1), generator=g, device=dev).to(torch.uint8).expand(total, n).contiguous()
-    elif args.workload == "config3" or args.actions == "random":
+    elif args.workload in ("config3", "config5") or args.actions == "random":
         g = torch.Generator(device=dev)
         g.manual_seed(1234 + rank)   # Philox counter-based RNG on the device
         acts = torch.randint(0, 8, (total, n), generator=g, device=dev, dtype=torch.int64).to(torch.uint8)
@@ -114,7 +136,7 @@ def main():
     torch.cuda.synchronize(dev)
 
     for t in range(args.warmup):
-        emu.step(acts[t])
+        env_step(t)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -123,12 +145,12 @@ def main():
     t0 = time.perf_counter()
     instr = 0
     for t in range(args.warmup, total):
-        emu.step(acts[t])
+        env_step(t)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    emu_ms, ren_ms, nprof = emu.profile_read()
+    emu_ms, ren_ms, rew_ms, nprof = emu.profile_read()
     instr = emu.last_instr_count()  # last step's emulated instructions (all envs)
     t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -139,6 +161,7 @@ def main():
         value = world * n * args.steps / elapsed
         k1_s = emu_ms / 1e3 / max(nprof, 1)
         k2_s = ren_ms / 1e3 / max(nprof, 1)
+        k4_s = rew_ms / 1e3 / max(nprof, 1)
         achieved = B_HEADLESS * n / k1_s / 1e9
         traffic = None
         prof_path = os.path.join(HERE, "profiles", f"pmc_{args.workload}.json")
@@ -161,9 +184,11 @@ def main():
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": ("configs[2]: 65536 envs/GPU, PPU-rendered 160x144 u8 screen obs, random actions"
-                             if args.workload == "config3" else
-                             "configs[1]: headless (no PPU), RAM-only obs, fixed action cycle [0,3,1,2]"),
+                "workload": {"config3": "configs[2]: 65536 envs/GPU, PPU-rendered 160x144 u8 screen obs, random actions",
+                             "config2": "configs[1]: headless (no PPU), RAM-only obs, fixed action cycle [0,3,1,2]",
+                             "config5": "configs[4]: configs[2] + full ram_map reward stack + (72,80,4) obs + "
+                                        "per-env template reload on done + episodic-return all-reduce every 128 steps",
+                             }[args.workload],
                 "envs_per_gpu": n,
                 "rom": rom_name,
                 "start_state": os.path.basename(args.state) if args.state else "power-on (post-boot)",
@@ -182,6 +207,7 @@ def main():
                 "bytes_per_env_step": B_HEADLESS,
                 "k1_ms": round(k1_s * 1e3, 3),
                 "k2_render_ms": round(k2_s * 1e3, 3),
+                "k4_reward_obs_ms": round(k4_s * 1e3, 3),
             },
             "emulated_instr_per_s": round(instr / max(k1_s, 1e-9), 1),
             "instr_per_env_step": round(instr / n, 1),

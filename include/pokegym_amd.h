@@ -19,6 +19,12 @@
  *   pk_snapshot      PyBoy save_state (v9 format)      environment.py:208-214
  *   pk_load_env      PyBoy load_state for one env      pyboy_binding.py:66-69
  *   pk_destroy       Env.close                         environment.py:412-413
+ *   pk_obs_ptr       Env.render (72,80,4) observation  environment.py:256-274, :233-254
+ *   pk_error_ptr     exceptions the reference raises   environment.py:739,744,568/580,1519,676
+ *   pk_get_ram       per-env RAM views (RAM-only obs)  ram_map.py:1768-1770 (batched)
+ *   pk_set_ram       per-env RAM writes                ram_map.py:1772-1774 (batched)
+ * With PK_F_REWARD, pk_step also runs the reward stack of Environment.step
+ * (environment.py:1338-1612) and pk_reset follows Environment.reset (:1233-1334).
  */
 #ifndef POKEGYM_AMD_H
 #define POKEGYM_AMD_H
@@ -29,13 +35,27 @@
 extern "C" {
 #endif
 
-#define PK_ABI_VERSION 1
+#define PK_ABI_VERSION 2
 #define PK_STATE_V9_BYTES 142610u
 #define PK_SCREEN_ROWS 144u
 #define PK_SCREEN_COLS 160u
 
 /* flags */
-#define PK_F_RENDER 1u /* rasterise the last frame of every step into the screen obs */
+#define PK_F_RENDER 1u          /* rasterise the last frame of every step into the screen obs */
+#define PK_F_REWARD 2u          /* reward stack + (72,80,4) obs + reference reset semantics */
+#define PK_F_RELOAD_ON_RESET 4u /* reload the template state on EVERY reset (the reference
+                                   reloads only on an env's first reset, environment.py:1241) */
+
+/* per-env error codes (pk_error_ptr): where the reference's step/reset raises, the env stops
+ * (reward 0, state frozen) and reports which exception the reference would have raised */
+#define PK_ERR_NONE 0
+#define PK_ERR_MAP_KEY 1        /* KeyError, MAP_ID_REF lookup (environment.py:739) */
+#define PK_ERR_STUCK_ATTR 2     /* AttributeError, stuck_cnt read before assignment (:744) */
+#define PK_ERR_MOVE_INDEX 3     /* IndexError, moves_obtained[move >= 0xA5] (:568, :580) */
+#define PK_ERR_CUT_COORDS 4     /* UnboundLocalError, cut coords for an unknown facing (:1519) */
+#define PK_ERR_HEATMAP_INDEX 5  /* IndexError, counts_map outside 444x436 (:676) */
+#define PK_ERR_BUS_INDEX 6      /* IndexError, memory read past 0xFFFF (box scan, :574-578) */
+#define PK_ERR_CAPACITY 7       /* device table full (no reference equivalent) */
 
 typedef struct pk_config {
     uint32_t n_envs;             /* envs on this GPU */
@@ -48,6 +68,7 @@ typedef struct pk_config {
     uint32_t release_frame;      /* button released before this frame; pokegym: 8 (:80) */
     uint32_t flags;              /* PK_F_* */
     uint32_t max_episode_steps;  /* truncation horizon; pokegym default 20480 (environment.py:1233) */
+    double reward_scale;         /* reset(reward_scale=4.0) (environment.py:1233); 0 = 4.0 */
 } pk_config;
 
 typedef struct pk_handle pk_handle;
@@ -57,8 +78,10 @@ void pk_destroy(pk_handle* h);
 const char* pk_last_error(void);
 int pk_abi_version(void);
 
-/* Reset envs whose env_mask_dev[e] != 0 (device u8[n]; NULL = all) to the template state and
- * zero their step counters. */
+/* Reset envs whose env_mask_dev[e] != 0 (device u8[n]; NULL = all).  Without PK_F_REWARD:
+ * reload the template state and zero the step counter.  With PK_F_REWARD: Environment.reset —
+ * D778 |= 0x10, template reload on the env's first reset only (or always with
+ * PK_F_RELOAD_ON_RESET), fresh episode bookkeeping, and the reset observation in pk_obs_ptr(). */
 int pk_reset(pk_handle* h, const uint8_t* env_mask_dev, void* stream);
 
 /* One env-step for all envs.
@@ -66,7 +89,7 @@ int pk_reset(pk_handle* h, const uint8_t* env_mask_dev, void* stream);
  *                 (pyboy_binding.py:40 ACTIONS); 8 = press nothing (extension).
  *   screen_dev  : optional device u8[n][144][160] copy of the grey screen (0xFF/0x99/0x55/0x00);
  *                 the handle's own persistent buffer is pk_screen_ptr().  NULL = no copy.
- *   rew_dev     : optional device f64[n]; reward (0 until the reward stack is enabled).
+ *   rew_dev     : optional device f64[n]; the step reward (PK_F_REWARD; 0 otherwise).
  *   term_dev / trunc_dev : optional device u8[n]; time >= max_episode_steps
  *                 (environment.py:1612-1613: terminated = truncated = done). */
 int pk_step(pk_handle* h, const uint8_t* actions_dev, uint8_t* screen_dev, double* rew_dev,
@@ -74,6 +97,15 @@ int pk_step(pk_handle* h, const uint8_t* actions_dev, uint8_t* screen_dev, doubl
 
 /* device pointer to the persistent u8[n][144][160] grey screen */
 uint8_t* pk_screen_ptr(pk_handle* h);
+/* device pointer to the u8[n][72][80][4] observation (PK_F_REWARD), updated by pk_step/pk_reset */
+uint8_t* pk_obs_ptr(pk_handle* h);
+/* device pointer to u32[n] PK_ERR_* codes (PK_F_REWARD), sticky until the env's next reset */
+const uint32_t* pk_error_ptr(pk_handle* h);
+
+/* Stream-ordered bulk RAM access for all envs: dense_dev[e * len + i] <-> guest address
+ * addr + i of env e.  RAM regions only (0xC000-0xFDFF incl. echo, 0xFF80-0xFFFE). */
+int pk_get_ram(pk_handle* h, uint16_t addr, uint32_t len, uint8_t* dense_dev, void* stream);
+int pk_set_ram(pk_handle* h, uint16_t addr, uint32_t len, const uint8_t* dense_dev, void* stream);
 uint32_t pk_num_envs(const pk_handle* h);
 
 /* Synchronous host-side accessors (parity tests, reward host mirrors, debugging). */
@@ -85,11 +117,12 @@ int pk_load_env(pk_handle* h, uint32_t env, const uint8_t* host_v9, uint64_t len
 /* Emulated instructions executed by the last pk_step, summed over envs (synchronous). */
 int pk_last_instr_count(pk_handle* h, uint64_t* out);
 
-/* Kernel timing with HIP events recorded on the step's stream around K1 (emulate) and K2
- * (render) of every pk_step while enabled.  pk_profile_read synchronises, returns the summed
- * milliseconds and the number of profiled steps since the last read, and resets the sums. */
+/* Kernel timing with HIP events recorded on the step's stream around K1 (emulate), K2 (render)
+ * and K4+K3 (reward + obs) of every pk_step while enabled.  pk_profile_read synchronises,
+ * returns the summed milliseconds and the number of profiled steps since the last read, and
+ * resets the sums. */
 int pk_profile_enable(pk_handle* h, int on);
-int pk_profile_read(pk_handle* h, double* emulate_ms, double* render_ms, uint64_t* steps);
+int pk_profile_read(pk_handle* h, double* emulate_ms, double* render_ms, double* reward_ms, uint64_t* steps);
 
 #ifdef __cplusplus
 }

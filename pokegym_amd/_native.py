@@ -11,14 +11,22 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libpokegym_amd.so")
 
+ABI_VERSION = 2
 PK_F_RENDER = 1
+PK_F_REWARD = 2
+PK_F_RELOAD_ON_RESET = 4
+OBS_SHAPE = (72, 80, 4)
+# PK_ERR_* -> the exception the reference raises at that point (include/pokegym_amd.h)
+ERR_EXCEPTIONS = {1: KeyError, 2: AttributeError, 3: IndexError, 4: UnboundLocalError, 5: IndexError,
+                  6: IndexError, 7: MemoryError}
 STATE_V9_BYTES = 142610
 ROWS, COLS = 144, 160
 
 # the exported symbols declared in include/pokegym_amd.h
 EXPORTS = ("pk_create", "pk_destroy", "pk_last_error", "pk_abi_version", "pk_reset", "pk_step",
            "pk_screen_ptr", "pk_num_envs", "pk_peek", "pk_poke", "pk_snapshot", "pk_load_env",
-           "pk_last_instr_count", "pk_profile_enable", "pk_profile_read")
+           "pk_last_instr_count", "pk_profile_enable", "pk_profile_read", "pk_obs_ptr", "pk_error_ptr",
+           "pk_get_ram", "pk_set_ram")
 
 
 class PkConfig(ctypes.Structure):
@@ -33,6 +41,7 @@ class PkConfig(ctypes.Structure):
         ("release_frame", ctypes.c_uint32),
         ("flags", ctypes.c_uint32),
         ("max_episode_steps", ctypes.c_uint32),
+        ("reward_scale", ctypes.c_double),
     ]
 
 
@@ -71,9 +80,22 @@ def load(path: str = LIB_PATH):
     L.pk_last_instr_count.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     L.pk_profile_enable.argtypes = [vp, ctypes.c_int]
     dp = ctypes.POINTER(ctypes.c_double)
-    L.pk_profile_read.argtypes = [vp, dp, dp, ctypes.POINTER(ctypes.c_uint64)]
+    L.pk_profile_read.argtypes = [vp, dp, dp, dp, ctypes.POINTER(ctypes.c_uint64)]
+    bind_v2(L)
     _lib = L
     return L
+
+
+def bind_v2(L):
+    """argtypes of the ABI-v2 entry points (shared with the host-simulation test build)."""
+    vp = ctypes.c_void_p
+    L.pk_obs_ptr.argtypes = [vp]
+    L.pk_obs_ptr.restype = vp
+    L.pk_error_ptr.argtypes = [vp]
+    L.pk_error_ptr.restype = vp
+    L.pk_get_ram.argtypes = [vp, ctypes.c_uint16, ctypes.c_uint32, vp, vp]
+    L.pk_set_ram.argtypes = [vp, ctypes.c_uint16, ctypes.c_uint32, vp, vp]
+    L.pk_reset.argtypes = [vp, vp, vp]
 
 
 def check(rc: int, what: str):

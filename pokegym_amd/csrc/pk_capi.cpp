@@ -18,6 +18,7 @@
 #include "../../include/pokegym_amd.h"
 #include "pk_decode.h"
 #include "pk_layout.h"
+#include "pk_reward.h"
 
 hipError_t pk_launch_step(const PkStepArgs& a, hipStream_t s);
 hipError_t pk_launch_render(const PkStepArgs& a, hipStream_t s);
@@ -26,6 +27,12 @@ hipError_t pk_launch_gather_env(const uint8_t* mem, uint32_t env, uint8_t* out, 
 hipError_t pk_launch_scatter_env(uint8_t* mem, uint32_t env, const uint8_t* in, hipStream_t s);
 hipError_t pk_launch_done(const uint32_t* time_reg, uint32_t n, uint32_t max_steps, uint8_t* term,
                           uint8_t* trunc, double* rew, hipStream_t s);
+hipError_t pk_launch_reward(const PkRewardArgs& a, hipStream_t s);
+hipError_t pk_launch_rreset_pre(const PkRewardArgs& a, hipStream_t s);
+hipError_t pk_launch_rreset_post(const PkRewardArgs& a, hipStream_t s);
+hipError_t pk_launch_obs(const PkRewardArgs& a, hipStream_t s);
+hipError_t pk_launch_ram_copy(uint8_t* mem, uint8_t* dense, uint32_t n, uint32_t phys0, uint32_t len,
+                              uint32_t to_dense, hipStream_t s);
 
 namespace {
 
@@ -231,7 +238,17 @@ struct pk_handle {
     uint32_t nslots = 1;
     size_t lat_stride = 0;
     Template tmpl;
-    // profiling: 3 events per profiled step (start, after K1, after K2)
+    // reward stack (PK_F_REWARD), see pk_reward.h
+    uint32_t* rs = nullptr;
+    double* rsd = nullptr;
+    uint32_t* seen = nullptr;
+    uint32_t* mask = nullptr;
+    uint32_t* cutc = nullptr;
+    uint8_t* obs = nullptr;
+    uint8_t* reload = nullptr;
+    uint32_t cap_log2 = 0;
+    double reward_scale = 4.0;
+    // profiling: 4 events per profiled step (start, after K1, after K2, after K4+K3)
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
@@ -249,9 +266,13 @@ static int prof_event(pk_handle* h, hipStream_t s) {
 
 extern "C" {
 
+static int template_reset(pk_handle* h, const uint8_t* mask, void* stream);
+
 const char* pk_last_error(void) { return g_err.c_str(); }
 int pk_abi_version(void) { return PK_ABI_VERSION; }
 uint8_t* pk_screen_ptr(pk_handle* h) { return h ? h->screen : nullptr; }
+uint8_t* pk_obs_ptr(pk_handle* h) { return h ? h->obs : nullptr; }
+const uint32_t* pk_error_ptr(pk_handle* h) { return (h && h->rs) ? h->rs + (size_t)RS_ERR * h->npad : nullptr; }
 uint32_t pk_num_envs(const pk_handle* h) { return h ? h->n : 0; }
 
 void pk_destroy(pk_handle* h) {
@@ -259,7 +280,7 @@ void pk_destroy(pk_handle* h) {
     (void)hipSetDevice(h->device);
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     void* ptrs[] = {h->mem, h->regs, h->lat, h->screen, h->rom, h->rom16, h->bank_slot, h->slot_bank, h->dtab, h->t_mem, h->t_regs,
-                    h->t_lat, h->t_screen, h->scratch};
+                    h->t_lat, h->t_screen, h->scratch, h->rs, h->rsd, h->seen, h->mask, h->cutc, h->obs, h->reload};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete h;
@@ -278,7 +299,8 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     if (type == 0x00) mbc = 0;
     else if (type >= 0x0F && type <= 0x13) mbc = 3;
     else return fail(-ENOTSUP, "cartridge type 0x%02x not supported (ROM-only and MBC3 are)", type);
-    if (cfg->frame_skip == 0 || cfg->frame_skip > 1024) return fail(-EINVAL, "bad frame_skip");
+    // frame_skip 0 = no emulation (reward-stack replay tests drive RAM through pk_set_ram)
+    if (cfg->frame_skip > 1024) return fail(-EINVAL, "bad frame_skip");
 
     pk_handle* h = new pk_handle();
     h->device = cfg->device;
@@ -289,6 +311,10 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     h->release = cfg->release_frame;
     h->flags = cfg->flags;
     h->max_steps = cfg->max_episode_steps ? cfg->max_episode_steps : 20480;
+    h->reward_scale = cfg->reward_scale != 0.0 ? cfg->reward_scale : 4.0;
+    // seen-coordinate set: one entry per step at most, load factor <= 3/4
+    h->cap_log2 = 10;
+    while ((1ull << h->cap_log2) * 3 < ((uint64_t)h->max_steps + 2) * 4) h->cap_log2++;
     h->mbc = mbc;
     h->bank_mask = banks - 1;
     h->lat_stride = (size_t)h->ngroups * PK_ROWS * PK_LANES;
@@ -321,6 +347,15 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     ALLOC(h->t_lat, 3 * PK_ROWS * 4);
     ALLOC(h->t_screen, PK_SCREEN);
     ALLOC(h->scratch, PK_PHYS + PK_NREGS * 4 + 3 * PK_ROWS * 4 + PK_SCREEN);
+    if (h->flags & PK_F_REWARD) {
+        ALLOC(h->rs, (size_t)RS_NFIELDS * h->npad * 4);
+        ALLOC(h->rsd, (size_t)RSD_NFIELDS * h->npad * 8);
+        ALLOC(h->seen, (size_t)h->npad * (1ull << h->cap_log2) * 4);
+        ALLOC(h->mask, (size_t)h->npad * PK_MASK_WORDS * 4);
+        ALLOC(h->cutc, (size_t)h->npad * PK_CUTC_CAP * 4);
+        ALLOC(h->obs, (size_t)h->npad * PK_OBS_BYTES);
+        ALLOC(h->reload, h->npad);
+    }
 #undef ALLOC
     uint32_t dt[1024];
     pk_build_dtab(dt);
@@ -352,24 +387,81 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     if (e == hipSuccess) e = hipMemcpy(h->t_screen, h->tmpl.screen.data(), PK_SCREEN, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemset(h->regs, 0, (size_t)PK_NREGS * h->npad * 4);
     if (e == hipSuccess) e = hipMemset(h->lat, 0, 3 * h->lat_stride * 4);
+    if (h->flags & PK_F_REWARD) {
+        // nothing has been reset yet (reset_count 0); update_heat_map's last_map = -1 (:462)
+        if (e == hipSuccess) e = hipMemset(h->rs, 0, (size_t)RS_NFIELDS * h->npad * 4);
+        if (e == hipSuccess) e = hipMemset(h->rs + (size_t)RS_HEAT_LAST * h->npad, 0xFF, (size_t)h->npad * 4);
+        if (e == hipSuccess) e = hipMemset(h->rs + (size_t)RS_MASK_MAP * h->npad, 0xFF, (size_t)h->npad * 4);
+        if (e == hipSuccess) e = hipMemset(h->rsd, 0, (size_t)RSD_NFIELDS * h->npad * 8);
+        if (e == hipSuccess) e = hipMemset(h->seen, 0, (size_t)h->npad * (1ull << h->cap_log2) * 4);
+        if (e == hipSuccess) e = hipMemset(h->mask, 0, (size_t)h->npad * PK_MASK_WORDS * 4);
+        if (e == hipSuccess) e = hipMemset(h->obs, 0, (size_t)h->npad * PK_OBS_BYTES);
+    }
     if (e != hipSuccess) {
         pk_destroy(h);
         return fail(-EIO, "device upload failed: %s", hipGetErrorString(e));
     }
-    if ((rc = pk_reset(h, nullptr, nullptr))) { pk_destroy(h); return rc; }
+    if ((rc = template_reset(h, nullptr, nullptr))) { pk_destroy(h); return rc; }
     if (hipDeviceSynchronize() != hipSuccess) { pk_destroy(h); return fail(-EIO, "initial reset failed"); }
     *out = h;
     return 0;
 }
 
-int pk_reset(pk_handle* h, const uint8_t* mask, void* stream) {
-    if (!h) return fail(-EINVAL, "null handle");
+static PkRewardArgs reward_args(pk_handle* h) {
+    PkRewardArgs r;
+    memset(&r, 0, sizeof r);
+    r.mem = h->mem; r.regs = h->regs; r.rs = h->rs; r.rsd = h->rsd; r.seen = h->seen; r.mask = h->mask;
+    r.cutc = h->cutc; r.reload = h->reload; r.screen = h->screen; r.obs = h->obs;
+    r.reward_scale = h->reward_scale; r.n = h->n; r.npad = h->npad; r.cap_log2 = h->cap_log2;
+    r.max_steps = h->max_steps; r.reload_always = (h->flags & PK_F_RELOAD_ON_RESET) ? 1 : 0;
+    return r;
+}
+
+// reload the template state (regs, RAM image, latches, screen) into the masked envs
+static int template_reset(pk_handle* h, const uint8_t* mask, void* stream) {
     HIPCHK(hipSetDevice(h->device));
     PkResetArgs a;
     a.mem = h->mem; a.regs = h->regs; a.lat = h->lat; a.screen = h->screen;
     a.tmpl_mem = h->t_mem; a.tmpl_regs = h->t_regs; a.tmpl_lat = h->t_lat; a.tmpl_screen = h->t_screen;
     a.mask = mask; a.n = h->n; a.npad = h->npad; a.lat_stride = (uint32_t)h->lat_stride;
     HIPCHK(pk_launch_reset(a, (hipStream_t)stream));
+    return 0;
+}
+
+int pk_reset(pk_handle* h, const uint8_t* mask, void* stream) {
+    if (!h) return fail(-EINVAL, "null handle");
+    if (!(h->flags & PK_F_REWARD)) return template_reset(h, mask, stream);
+    HIPCHK(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    PkRewardArgs r = reward_args(h);
+    r.env_mask = mask;
+    HIPCHK(pk_launch_rreset_pre(r, s));
+    int rc = template_reset(h, h->reload, stream);
+    if (rc) return rc;
+    HIPCHK(pk_launch_rreset_post(r, s));
+    HIPCHK(pk_launch_obs(r, s));
+    return 0;
+}
+
+int pk_get_ram(pk_handle* h, uint16_t addr, uint32_t len, uint8_t* dense, void* stream) {
+    if (!h || !dense) return fail(-EINVAL, "null argument");
+    bool wram = addr >= 0xC000 && (uint32_t)addr + len <= 0xFE00, hram = addr >= 0xFF80 && (uint32_t)addr + len <= 0xFFFF;
+    if (!len || !(wram || hram)) return fail(-EINVAL, "pk_get_ram: [0x%04x, +%u) is not inside WRAM/echo or HRAM", addr, len);
+    if (wram && (addr & 0x1FFF) + len > 0x2000) return fail(-EINVAL, "pk_get_ram: range wraps the echo mirror");
+    HIPCHK(hipSetDevice(h->device));
+    uint32_t phys0 = wram ? PK_P_WRAM + (addr & 0x1FFFu) : PK_P_HRAM + (addr - 0xFF80u);
+    HIPCHK(pk_launch_ram_copy(h->mem, dense, h->n, phys0, len, 1, (hipStream_t)stream));
+    return 0;
+}
+
+int pk_set_ram(pk_handle* h, uint16_t addr, uint32_t len, const uint8_t* dense, void* stream) {
+    if (!h || !dense) return fail(-EINVAL, "null argument");
+    bool wram = addr >= 0xC000 && (uint32_t)addr + len <= 0xFE00, hram = addr >= 0xFF80 && (uint32_t)addr + len <= 0xFFFF;
+    if (!len || !(wram || hram)) return fail(-EINVAL, "pk_set_ram: [0x%04x, +%u) is not inside WRAM/echo or HRAM", addr, len);
+    if (wram && (addr & 0x1FFF) + len > 0x2000) return fail(-EINVAL, "pk_set_ram: range wraps the echo mirror");
+    HIPCHK(hipSetDevice(h->device));
+    uint32_t phys0 = wram ? PK_P_WRAM + (addr & 0x1FFFu) : PK_P_HRAM + (addr - 0xFF80u);
+    HIPCHK(pk_launch_ram_copy(h->mem, const_cast<uint8_t*>(dense), h->n, phys0, len, 0, (hipStream_t)stream));
     return 0;
 }
 
@@ -392,10 +484,17 @@ int pk_step(pk_handle* h, const uint8_t* actions, uint8_t* screen_out, double* r
     if (h->prof && (rc = prof_event(h, s))) return rc;
     if (a.render_last) HIPCHK(pk_launch_render(a, s));
     if (h->prof && (rc = prof_event(h, s))) return rc;
+    if (h->flags & PK_F_REWARD) {
+        PkRewardArgs r = reward_args(h);
+        r.actions = actions; r.rew = rew; r.term = term; r.trunc = trunc;
+        HIPCHK(pk_launch_reward(r, s));
+        HIPCHK(pk_launch_obs(r, s));
+    } else if (rew || term || trunc) {
+        HIPCHK(pk_launch_done(h->regs + (size_t)PK_R_TIME * h->npad, h->n, h->max_steps, term, trunc, rew, s));
+    }
+    if (h->prof && (rc = prof_event(h, s))) return rc;
     if (screen_out)
         HIPCHK(hipMemcpyAsync(screen_out, h->screen, (size_t)h->n * PK_SCREEN, hipMemcpyDeviceToDevice, s));
-    if (rew || term || trunc)
-        HIPCHK(pk_launch_done(h->regs + (size_t)PK_R_TIME * h->npad, h->n, h->max_steps, term, trunc, rew, s));
     return 0;
 }
 
@@ -556,21 +655,24 @@ int pk_profile_enable(pk_handle* h, int on) {
     return 0;
 }
 
-int pk_profile_read(pk_handle* h, double* emu_ms, double* render_ms, uint64_t* steps) {
-    if (!h || !emu_ms || !render_ms || !steps) return fail(-EINVAL, "null argument");
+int pk_profile_read(pk_handle* h, double* emu_ms, double* render_ms, double* reward_ms, uint64_t* steps) {
+    if (!h || !emu_ms || !render_ms || !reward_ms || !steps) return fail(-EINVAL, "null argument");
     HIPCHK(hipSetDevice(h->device));
-    double a = 0, b = 0;
-    size_t n = h->ev_used / 3;
+    double a = 0, b = 0, c = 0;
+    size_t n = h->ev_used / 4;
     if (n) HIPCHK(hipEventSynchronize(h->ev_pool[h->ev_used - 1]));
     for (size_t i = 0; i < n; i++) {
-        float t1 = 0, t2 = 0;
-        HIPCHK(hipEventElapsedTime(&t1, h->ev_pool[3 * i], h->ev_pool[3 * i + 1]));
-        HIPCHK(hipEventElapsedTime(&t2, h->ev_pool[3 * i + 1], h->ev_pool[3 * i + 2]));
+        float t1 = 0, t2 = 0, t3 = 0;
+        HIPCHK(hipEventElapsedTime(&t1, h->ev_pool[4 * i], h->ev_pool[4 * i + 1]));
+        HIPCHK(hipEventElapsedTime(&t2, h->ev_pool[4 * i + 1], h->ev_pool[4 * i + 2]));
+        HIPCHK(hipEventElapsedTime(&t3, h->ev_pool[4 * i + 2], h->ev_pool[4 * i + 3]));
         a += t1;
         b += t2;
+        c += t3;
     }
     *emu_ms = a;
     *render_ms = b;
+    *reward_ms = c;
     *steps = n;
     h->ev_used = 0;
     return 0;

@@ -3,7 +3,9 @@
 This is the device-side replacement of pokegym's per-process PyBoy instance
 (pokegym/pyboy_binding.py:42-91): one call to `step(actions)` advances every env by one
 env-step (press, 24 frames, release before frame 8, rasterise frame 24) inside one HIP launch.
-Device buffers are PyTorch-ROCm tensors; the kernels run on the caller's current HIP stream.
+With `reward=True` the same call also runs pokegym's reward stack and builds the (72, 80, 4)
+observation (environment.py:1338-1612, :256-274) on the device.  Device buffers are
+PyTorch-ROCm tensors; the kernels run on the caller's current HIP stream.
 """
 from __future__ import annotations
 
@@ -13,7 +15,8 @@ import numpy as np
 import torch
 
 from . import _native
-from ._native import PK_F_RENDER, STATE_V9_BYTES, ROWS, COLS, check
+from ._native import (COLS, ERR_EXCEPTIONS, OBS_SHAPE, PK_F_RELOAD_ON_RESET, PK_F_RENDER, PK_F_REWARD, ROWS,
+                      STATE_V9_BYTES, check)
 
 
 class _CudaArray:
@@ -33,7 +36,8 @@ def _u8p(buf: bytes | bytearray | np.ndarray):
 class BatchedEmulator:
     def __init__(self, rom: bytes, n_envs: int, state: bytes | None = None, device: int = 0,
                  frame_skip: int = 24, release_frame: int = 8, render: bool = True,
-                 max_episode_steps: int = 20480):
+                 max_episode_steps: int = 20480, reward: bool = False, reload_on_reset: bool = False,
+                 reward_scale: float = 4.0):
         self._L = _native.load()
         if not torch.cuda.is_available():
             raise _native.PkError("no ROCm GPU visible: the HIP path has no CPU fallback")
@@ -51,15 +55,25 @@ class BatchedEmulator:
             cfg.state_len = len(self._state)
         cfg.frame_skip = frame_skip
         cfg.release_frame = release_frame
-        cfg.flags = PK_F_RENDER if render else 0
+        cfg.flags = ((PK_F_RENDER if render else 0) | (PK_F_REWARD if reward else 0)
+                     | (PK_F_RELOAD_ON_RESET if reload_on_reset else 0))
         cfg.max_episode_steps = max_episode_steps
+        cfg.reward_scale = reward_scale
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             check(self._L.pk_create(ctypes.byref(cfg), ctypes.byref(h)), "pk_create")
         self._h = h
         self.render = render
+        self.reward = reward
         ptr = self._L.pk_screen_ptr(self._h)
         self.screen = torch.as_tensor(_CudaArray(ptr, (self.n, ROWS, COLS), "|u1"), device=self.device)
+        self.obs = None
+        self.errors = None
+        if reward:
+            self.obs = torch.as_tensor(_CudaArray(self._L.pk_obs_ptr(self._h), (self.n,) + OBS_SHAPE, "|u1"),
+                                       device=self.device)
+            self.errors = torch.as_tensor(_CudaArray(self._L.pk_error_ptr(self._h), (self.n,), "<i4"),
+                                          device=self.device)
         self.rewards = torch.zeros(self.n, dtype=torch.float64, device=self.device)
         self.terminals = torch.zeros(self.n, dtype=torch.uint8, device=self.device)
         self.truncations = torch.zeros(self.n, dtype=torch.uint8, device=self.device)
@@ -70,7 +84,8 @@ class BatchedEmulator:
 
     # -- hot path -----------------------------------------------------------------------
     def step(self, actions: torch.Tensor):
-        """actions: uint8[n] on this device. Returns (screen, rewards, terminals, truncations)."""
+        """actions: uint8[n] on this device.  Returns (obs, rewards, terminals, truncations) where
+        obs is the (n, 72, 80, 4) observation with reward=True, else the (n, 144, 160) screen."""
         if actions.dtype != torch.uint8 or actions.device != self.device or actions.numel() != self.n:
             raise ValueError("actions must be a uint8 tensor of n_envs elements on the emulator's device")
         actions = actions.contiguous()
@@ -78,11 +93,39 @@ class BatchedEmulator:
                               ctypes.c_void_p(self.rewards.data_ptr()),
                               ctypes.c_void_p(self.terminals.data_ptr()),
                               ctypes.c_void_p(self.truncations.data_ptr()), self._stream()), "pk_step")
-        return self.screen, self.rewards, self.terminals, self.truncations
+        return (self.obs if self.reward else self.screen), self.rewards, self.terminals, self.truncations
 
     def reset(self, mask: torch.Tensor | None = None):
-        mp = None if mask is None else ctypes.c_void_p(mask.to(torch.uint8).contiguous().data_ptr())
+        """Reset all envs (mask None) or those with mask[e] != 0 (device tensor).  Returns the obs."""
+        mp = None
+        if mask is not None:
+            mask = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+            mp = ctypes.c_void_p(mask.data_ptr())
         check(self._L.pk_reset(self._h, mp, self._stream()), "pk_reset")
+        return self.obs if self.reward else self.screen
+
+    def raise_if_failed(self, env: int | None = None):
+        """Raise the exception the reference would have raised for a failed env (PK_ERR_*)."""
+        if self.errors is None:
+            return
+        err = self.errors if env is None else self.errors[env:env + 1]
+        bad = torch.nonzero(err).flatten()
+        if bad.numel():
+            e = int(bad[0]) + (0 if env is None else env)
+            code = int(self.errors[e])
+            raise ERR_EXCEPTIONS.get(code, RuntimeError)(f"env {e}: reference reward stack raises here (PK_ERR {code})")
+
+    # -- bulk RAM views (stream-ordered) ------------------------------------------------
+    def get_ram(self, addr: int, length: int, out: torch.Tensor | None = None) -> torch.Tensor:
+        if out is None:
+            out = torch.empty((self.n, length), dtype=torch.uint8, device=self.device)
+        check(self._L.pk_get_ram(self._h, addr, length, ctypes.c_void_p(out.data_ptr()), self._stream()), "pk_get_ram")
+        return out
+
+    def set_ram(self, addr: int, data: torch.Tensor):
+        data = data.to(device=self.device, dtype=torch.uint8).contiguous()
+        length = data.numel() // self.n
+        check(self._L.pk_set_ram(self._h, addr, length, ctypes.c_void_p(data.data_ptr()), self._stream()), "pk_set_ram")
 
     # -- host-side accessors (synchronous) --------------------------------------------
     def snapshot(self, env: int) -> bytes:
@@ -113,15 +156,18 @@ class BatchedEmulator:
         check(self._L.pk_profile_enable(self._h, 1 if on else 0), "pk_profile_enable")
 
     def profile_read(self):
-        """(emulate_ms_total, render_ms_total, steps) since the last read (synchronous)."""
-        a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
-        check(self._L.pk_profile_read(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)), "pk_profile_read")
-        return a.value, b.value, int(n.value)
+        """(emulate_ms, render_ms, reward_ms, steps) summed since the last read (synchronous)."""
+        a, b, c, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
+        check(self._L.pk_profile_read(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c), ctypes.byref(n)),
+              "pk_profile_read")
+        return a.value, b.value, c.value, int(n.value)
 
     def close(self):
         if getattr(self, "_h", None):
             torch.cuda.synchronize(self.device)
             self.screen = None
+            self.obs = None
+            self.errors = None
             self._L.pk_destroy(self._h)
             self._h = None
 

@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <barrier>
 #include <functional>
 #include <thread>
@@ -24,6 +25,8 @@
 #define __noinline__ __attribute__((noinline))
 #define __launch_bounds__(...)
 #define __builtin_amdgcn_readfirstlane(x) (x)
+using std::max;
+using std::min;
 
 struct dim3 {
     unsigned x, y, z;
@@ -64,9 +67,9 @@ static inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuc
 static inline hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
 static inline hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) { *ms = 0.f; return hipSuccess; }
 
-void pk_sim_launch(dim3 grid, dim3 block, const std::function<void()>& body);
+void pk_sim_launch(const char* name, dim3 grid, dim3 block, const std::function<void()>& body);
 #define hipLaunchKernelGGL(k, grid, block, shmem, stream, ...) \
-    pk_sim_launch(dim3(grid), dim3(block), [&]() { k(__VA_ARGS__); })
+    pk_sim_launch(#k, dim3(grid), dim3(block), [&]() { k(__VA_ARGS__); })
 
 // instruction trace for debugging (env, pc, w0, w1, sp, opcode)
 extern "C" void pk_sim_trace(uint32_t env, uint32_t pc, uint32_t w0, uint32_t w1, uint32_t sp, uint32_t op);

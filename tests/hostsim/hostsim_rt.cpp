@@ -7,7 +7,31 @@ dim3 blockDim;
 dim3 gridDim;
 std::barrier<>* pk_sim_barrier = nullptr;
 
-void pk_sim_launch(dim3 grid, dim3 block, const std::function<void()>& body) {
+// Kernels that never call __syncthreads run without barriers: a few workers take whole blocks
+// and run their threads one after another.
+static void launch_independent(dim3 grid, dim3 block, const std::function<void()>& body) {
+    gridDim = grid;
+    blockDim = block;
+    const unsigned nw = 8;
+    std::vector<std::thread> ts;
+    for (unsigned w = 0; w < nw; w++)
+        ts.emplace_back([&, w]() {
+            for (unsigned b = w; b < grid.x; b += nw) {
+                blockIdx = dim3(b);
+                for (unsigned t = 0; t < block.x; t++) {
+                    threadIdx = dim3(t);
+                    body();
+                }
+            }
+        });
+    for (auto& th : ts) th.join();
+}
+
+void pk_sim_launch(const char* name, dim3 grid, dim3 block, const std::function<void()>& body) {
+    if (strcmp(name, "pk_step_kernel") != 0) {  // the only kernel with __shared__ + __syncthreads
+        launch_independent(grid, block, body);
+        return;
+    }
     // blockDim.x OS threads walk the blocks in order; a barrier at the end of every block keeps
     // the per-block __shared__ statics private to the block being run.
     gridDim = grid;

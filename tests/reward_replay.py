@@ -50,3 +50,72 @@ def obs_hash(o):
 def writes_of(g, row):
     a, b = g["diff_ptr"][row], g["diff_ptr"][row + 1]
     return list(zip(g["diff_addr"][a:b].tolist(), g["diff_val"][a:b].tolist()))
+
+
+# ---------------------------------------------------------------------------------------------
+# driving a C-ABI implementation (host-simulation build or the real HIP library)
+STATE_WRAM, STATE_HRAM, STATE_SCREEN = 101285, 109649, 9125
+
+
+def template_state(base_state: bytes, w, h, screen):
+    """A v9 state = base_state with WRAM/HRAM/screen replaced (the reload source of pk_reset)."""
+    s = np.frombuffer(base_state, np.uint8).copy()
+    s[STATE_WRAM:STATE_WRAM + 8192] = w
+    s[STATE_HRAM:STATE_HRAM + 127] = h
+    px = s[STATE_SCREEN:STATE_SCREEN + 144 * 160 * 4].reshape(144 * 160, 4)
+    g = screen.reshape(-1)
+    px[:, 0] = (g == 0xFF)
+    px[:, 1] = px[:, 2] = px[:, 3] = g
+    return s.tobytes()
+
+
+def run_replay(backend, base_state: bytes, g, seqs):
+    """Replay every golden sequence through `backend` (one 1-env handle per sequence).
+    Returns the number of events checked; raises AssertionError on the first mismatch."""
+    from oracle.reward import ERR_NAMES
+    n_checked = 0
+    for si, (seed, steps, max_steps, allow_err), W, H, S, A, rows in seqs:
+        h = backend.create(template_state(base_state, W[0], H[0], S[0]), int(max_steps))
+        try:
+            t = 0
+            first = True
+            for row in rows:
+                kind, gt = int(g["kind"][row]), int(g["t"][row])
+                err = str(g["err"][row])
+                if kind == 0:
+                    if first:
+                        bw, bh = W[0], H[0]
+                    else:
+                        bw, bh = backend.get_ram(h)
+                    first = False
+                    backend.reset(h)
+                    e = backend.error(h)
+                    if err:
+                        assert e and ERR_NAMES.get(e) == err, (si, "reset", gt, err, e)
+                        break
+                    assert e == 0, (si, "reset", gt, e)
+                    assert obs_hash(backend.obs(h)) == str(g["obs_sha1"][row]), (si, "reset obs", gt)
+                else:
+                    t = gt
+                    backend.set_ram(h, W[t], H[t])
+                    backend.set_screen(h, S[t])
+                    bw, bh = W[t], H[t]
+                    r, d = backend.step(h, int(A[t - 1]))
+                    e = backend.error(h)
+                    if err:
+                        assert e and ERR_NAMES.get(e) == err, (si, t, err, e)
+                        break
+                    assert e == 0, (si, t, e)
+                    assert r == float(g["reward"][row]), (si, t, r, float(g["reward"][row]))
+                    assert int(d) == int(g["done"][row]), (si, t)
+                    assert obs_hash(backend.obs(h)) == str(g["obs_sha1"][row]), (si, "step obs", t)
+                w2, h2 = backend.get_ram(h)
+                got = {0xC000 + int(a): int(w2[a]) for a in np.nonzero(w2 != bw)[0]}
+                got.update({0xFF80 + int(a): int(h2[a]) for a in np.nonzero(h2 != bh)[0]})
+                a0, a1 = g["diff_ptr"][row], g["diff_ptr"][row + 1]
+                exp = dict(zip(g["diff_addr"][a0:a1].tolist(), g["diff_val"][a0:a1].tolist()))
+                assert got == exp, (si, gt, {hex(a): v for a, v in got.items()}, {hex(a): v for a, v in exp.items()})
+                n_checked += 1
+        finally:
+            backend.destroy(h)
+    return n_checked

@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(path)
     for sym in _declared():
         assert hasattr(lib, sym), sym
-    assert lib.pk_abi_version() == 1
+    assert lib.pk_abi_version() == _native.ABI_VERSION
 
 
 def test_create_without_gpu_fails_loudly():

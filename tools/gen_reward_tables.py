@@ -165,7 +165,9 @@ def main():
     # ---- C header
     h = ["// pk_reward_tables.h — GENERATED by tools/gen_reward_tables.py (probing the reference's",
          "// reward functions on a fake bus; see that script for the file:line of each table).",
-         "#pragma once", "#include <stdint.h>", ""]
+         "#pragma once", "#include <stdint.h>", "",
+         "// device-visible constant tables (the host-simulation build defines __constant__ away)",
+         "#define PK_TBL __device__ __constant__", ""]
     allm = []
     starts = []
     for name in MONITOR_NAMES:
@@ -175,12 +177,12 @@ def main():
     h.append(f"#define PK_NMON {len(MONITOR_NAMES)}")
     h.append(f"#define PK_NMON_ENT {len(allm)}")
     h.append("// monitors in order " + " ".join(MONITOR_NAMES) + "; entry = addr | bit<<16 | (weight+128)<<20")
-    h.append("static const uint16_t pk_mon_start[PK_NMON + 1] = {" + ", ".join(map(str, starts)) + "};")
-    h.append("static const uint32_t pk_mon_ent[PK_NMON_ENT] = {")
+    h.append("PK_TBL uint16_t pk_mon_start[PK_NMON + 1] = {" + ", ".join(map(str, starts)) + "};")
+    h.append("PK_TBL uint32_t pk_mon_ent[PK_NMON_ENT] = {")
     for a, b, w in allm:
         h.append(f"    0x{a | (b << 16) | ((w + 128) << 20):08X}u,")
     h.append("};")
-    h.append("static const int8_t pk_dojo_w[8] = {" + ", ".join(map(str, dojo_w)) + "};")
+    h.append("PK_TBL int8_t pk_dojo_w[8] = {" + ", ".join(map(str, dojo_w)) + "};")
     bits = []
     for t in BAG_TARGETS:
         words = [0] * 8
@@ -188,7 +190,7 @@ def main():
             words[v >> 5] |= 1 << (v & 31)
         bits.append("{" + ", ".join(f"0x{w:08X}u" for w in words) + "}")
     h.append("// item-id bitmaps whose bag name is " + ", ".join(BAG_TARGETS))
-    h.append("static const uint32_t pk_bag_name_bits[5][8] = {" + ", ".join(bits) + "};")
+    h.append("PK_TBL uint32_t pk_bag_name_bits[5][8] = {" + ", ".join(bits) + "};")
     mc = []
     for mid in range(256):
         if mid in map_coord:
@@ -197,7 +199,7 @@ def main():
         else:
             mc.append("{0, 0, 0}")
     h.append("// local_to_global offsets: {map_x, map_y, known}")
-    h.append("static const int16_t pk_map_coord[256][3] = {" + ", ".join(mc) + "};")
+    h.append("PK_TBL int16_t pk_map_coord[256][3] = {" + ", ".join(mc) + "};")
     md = []
     for mid in range(256):
         if mid in map_dims:
@@ -206,15 +208,15 @@ def main():
         else:
             md.append("{0, 0, 0}")
     h.append("// MAP_DICT dims via MAP_ID_REF: {height, width, known}")
-    h.append("static const int16_t pk_map_dims[256][3] = {" + ", ".join(md) + "};")
+    h.append("PK_TBL int16_t pk_map_dims[256][3] = {" + ", ".join(md) + "};")
     h.append(f"#define PK_NTREES {len(trees)}")
-    h.append("static const int16_t pk_trees[PK_NTREES][3] = {" + ", ".join(f"{{{m}, {x}, {y}}}" for m, x, y in trees) + "};")
+    h.append("PK_TBL int16_t pk_trees[PK_NTREES][3] = {" + ", ".join(f"{{{m}, {x}, {y}}}" for m, x, y in trees) + "};")
     h.append(f"#define PK_NMENU_LOC {len(menu_loc)}")
-    h.append("static const uint32_t pk_menu_loc[PK_NMENU_LOC] = {" +
+    h.append("PK_TBL uint32_t pk_menu_loc[PK_NMENU_LOC] = {" +
              ", ".join(f"0x{a | (b << 8) | (v << 16):06X}u" for a, b, v in menu_loc) + "};  // cc30 | cc31<<8 | value<<16")
     h.append(f"#define PK_NITEM_LOC {len(item_loc)}")
-    h.append("static const uint16_t pk_item_loc[PK_NITEM_LOC][2] = {" + ", ".join(f"{{{k}, {v}}}" for k, v in item_loc) + "};")
-    h.append("static const uint16_t pk_menu_item_keys[3] = {" + ", ".join(f"0x{a | (b << 8):04X}" for a, b in menu_item_keys) + "};")
+    h.append("PK_TBL uint16_t pk_item_loc[PK_NITEM_LOC][2] = {" + ", ".join(f"{{{k}, {v}}}" for k, v in item_loc) + "};")
+    h.append("PK_TBL uint16_t pk_menu_item_keys[3] = {" + ", ".join(f"0x{a | (b << 8):04X}" for a, b in menu_item_keys) + "};")
     for k, v in menu_consts.items():
         h.append(f"#define PK_{k} {v}")
     open(os.path.join(REPO, "pokegym_amd", "csrc", "pk_reward_tables.h"), "w").write("\n".join(h) + "\n")
