@@ -1,0 +1,68 @@
+"""Multi-GPU sharding of envs (one process per GPU) and the episode-statistics all-reduce.
+
+Envs are independent, so env.step has no data-path collective: rank g of W
+owns the contiguous env-id range shard_range(N, W, g) and runs it on its own GPU.  The only
+collective is the all-reduce (sum) of a few float64 episode statistics per logging interval —
+over RCCL/xGMI on MI355X (backend "nccl"), or gloo on CPU.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+STAT_FIELDS = ("episodic_return_sum", "episodes", "episode_length_sum", "reward_sum", "steps")
+
+
+def shard_range(num_envs: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous [start, end) env ids of `rank`; sizes differ by at most one."""
+    if not 0 <= rank < world:
+        raise ValueError(f"rank {rank} not in [0, {world})")
+    base, extra = divmod(num_envs, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def env_rank() -> tuple[int, int, int]:
+    """(rank, world, local_rank) from the torchrun environment (1 process = 1 GPU)."""
+    return int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+class EpisodeStats:
+    """Device-resident per-env episode accumulators + a 5-float64 summary all-reduced over ranks."""
+
+    def __init__(self, n: int, device):
+        self.device = torch.device(device)
+        self.ep_return = torch.zeros(n, dtype=torch.float64, device=self.device)
+        self.ep_length = torch.zeros(n, dtype=torch.float64, device=self.device)
+        self.summary = torch.zeros(len(STAT_FIELDS), dtype=torch.float64, device=self.device)
+
+    def update(self, rewards: torch.Tensor, done: torch.Tensor):
+        """Accumulate one step; finished episodes move into the summary (no host sync)."""
+        d = done.to(torch.float64)
+        self.ep_return.add_(rewards.to(torch.float64))
+        self.ep_length.add_(1.0)
+        s = self.summary
+        s[0] += (self.ep_return * d).sum()
+        s[1] += d.sum()
+        s[2] += (self.ep_length * d).sum()
+        s[3] += rewards.to(torch.float64).sum()
+        s[4] += float(rewards.numel())
+        keep = 1.0 - d
+        self.ep_return.mul_(keep)
+        self.ep_length.mul_(keep)
+
+    def allreduce(self, group=None) -> dict:
+        """Sum the summaries of all ranks (RCCL over xGMI when the tensors live on GPUs)."""
+        out = self.summary.clone()
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
+        vals = out.tolist()
+        res = dict(zip(STAT_FIELDS, vals))
+        res["mean_episodic_return"] = vals[0] / vals[1] if vals[1] else float("nan")
+        res["mean_episode_length"] = vals[2] / vals[1] if vals[1] else float("nan")
+        return res
+
+    def reset_summary(self):
+        self.summary.zero_()

@@ -1,0 +1,148 @@
+"""Gymnasium- and PufferLib-shaped surfaces over the batched MI355X env.step.
+
+`Environment` is the drop-in for pokegym.environment.Environment (environment.py:436-1812): same
+constructor arguments, reset(seed, options, max_episode_steps, reward_scale) -> (obs, info),
+step(action) -> (obs, reward, terminated, truncated, info), close(); observation (72, 80, 4) u8,
+Discrete(8) actions.  Where the reference raises inside step/reset, the same exception type is
+raised here (the device reports it per env, include/pokegym_amd.h PK_ERR_*).
+
+`VecEnv` is the PufferLib-style batch of N envs on ONE GPU (the intended way to use the device):
+reset(seed) -> (obs, infos); step(actions) -> (obs, rewards, terminals, truncations, infos);
+async_reset/send/recv; single_observation_space, single_action_space, num_envs.  Finished envs
+are reset inside step (their returned obs is the first obs of the next episode), stream-ordered
+with no host synchronisation; episode statistics are accumulated on the device and all-reduced
+across ranks every `log_interval` steps (pokegym_amd.dist).  For several GPUs, run one process
+per GPU and build each rank's shard with `make_sharded_vecenv`.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from . import spaces
+from .dist import EpisodeStats, env_rank, shard_range
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+DEFAULT_STATE = os.path.join(HERE, "states", "Bulbasaur.state")  # environment.py:119-120
+
+
+def _read(path_or_bytes):
+    if path_or_bytes is None or isinstance(path_or_bytes, (bytes, bytearray)):
+        return path_or_bytes
+    with open(path_or_bytes, "rb") as f:
+        return f.read()
+
+
+class Environment:
+    """One env (a single emulator lane).  Functionally the reference env; for throughput use
+    VecEnv, which steps thousands of envs per kernel launch."""
+
+    def __init__(self, rom_path="pokemon_red.gb", state_path=None, headless=True, save_video=False, quiet=False,
+                 verbose=False, device: int = 0, max_episode_steps: int = 20480, reward_scale: float = 4.0, **kwargs):
+        from .emulator import BatchedEmulator
+        rom = _read(rom_path)
+        state = _read(state_path if state_path is not None else DEFAULT_STATE)
+        self.max_episode_steps, self.reward_scale = max_episode_steps, reward_scale
+        self.emu = BatchedEmulator(rom, 1, state=state, device=device, render=True, reward=True,
+                                   max_episode_steps=max_episode_steps, reward_scale=reward_scale)
+        self.observation_space = spaces.observation_space()
+        self.action_space = spaces.action_space()
+        self.headless = headless
+
+    def reset(self, seed=None, options=None, max_episode_steps=None, reward_scale=None):
+        """environment.py:1233-1334 (seeding is not supported, as in the reference)."""
+        if max_episode_steps not in (None, self.max_episode_steps) or reward_scale not in (None, self.reward_scale):
+            raise ValueError("max_episode_steps / reward_scale are fixed at construction on the device")
+        obs = self.emu.reset()
+        self.emu.raise_if_failed(0)
+        return obs[0].cpu().numpy(), {}
+
+    def step(self, action, fast_video=True):
+        """environment.py:1336-1812; info is {} (the reference fills it only at done / every 10k steps)."""
+        a = torch.tensor([int(action)], dtype=torch.uint8, device=self.emu.device)
+        obs, rew, term, trunc = self.emu.step(a)
+        self.emu.raise_if_failed(0)
+        done = bool(term[0].item())
+        return obs[0].cpu().numpy(), float(rew[0].item()), done, done, {}
+
+    def render(self):
+        return self.emu.obs[0].cpu().numpy()
+
+    def close(self):
+        self.emu.close()
+
+
+class VecEnv:
+    """N envs on one GPU with PufferLib-style batch semantics (device tensors in and out)."""
+
+    def __init__(self, num_envs: int, rom_path=None, state_path=None, rom: bytes | None = None, state: bytes | None = None,
+                 device: int | None = None, max_episode_steps: int = 20480, reward_scale: float = 4.0,
+                 reload_on_reset: bool = False, env_offset: int = 0, log_interval: int = 128, emulator=None):
+        if emulator is None:
+            from .emulator import BatchedEmulator
+            rom = rom if rom is not None else _read(rom_path or "pokemon_red.gb")
+            state = state if state is not None else _read(state_path if state_path is not None else DEFAULT_STATE)
+            emulator = BatchedEmulator(rom, num_envs, state=state, device=0 if device is None else device, render=True,
+                                       reward=True, max_episode_steps=max_episode_steps, reward_scale=reward_scale,
+                                       reload_on_reset=reload_on_reset)
+        self.emu = emulator
+        self.device = emulator.device
+        self.num_envs = self.num_agents = num_envs
+        self.single_observation_space = spaces.observation_space()
+        self.single_action_space = spaces.action_space()
+        self.env_ids = torch.arange(env_offset, env_offset + num_envs, device=self.device)
+        self.masks = torch.ones(num_envs, dtype=torch.bool, device=self.device)
+        self.stats = EpisodeStats(num_envs, self.device)
+        self.log_interval = log_interval
+        self.t = 0
+        self._pending = None
+
+    def reset(self, seed=None):
+        obs = self.emu.reset()
+        self.t = 0
+        return obs, []
+
+    def step(self, actions):
+        if isinstance(actions, np.ndarray):
+            actions = torch.from_numpy(actions)
+        a = actions.to(device=self.device, dtype=torch.uint8).contiguous()
+        obs, rew, term, trunc = self.emu.step(a)
+        rewards = rew.clone()
+        terminals = term.to(torch.bool)
+        truncations = trunc.to(torch.bool)
+        self.stats.update(rewards, term)
+        self.emu.reset(term)  # auto-reset finished envs (no host sync)
+        self.t += 1
+        infos = []
+        if self.log_interval and self.t % self.log_interval == 0:
+            if hasattr(self.emu, "raise_if_failed"):
+                self.emu.raise_if_failed()
+            infos = [self.stats.allreduce()]
+        return obs, rewards, terminals, truncations, infos
+
+    # PufferLib async API
+    def async_reset(self, seed=None):
+        obs, infos = self.reset(seed)
+        z = torch.zeros(self.num_envs, device=self.device)
+        f = torch.zeros(self.num_envs, dtype=torch.bool, device=self.device)
+        self._pending = (obs, z, f, f, infos)
+
+    def send(self, actions):
+        self._pending = self.step(actions)
+
+    def recv(self):
+        obs, rew, term, trunc, infos = self._pending
+        return obs, rew, term, trunc, infos, self.env_ids, self.masks
+
+    def close(self):
+        self.emu.close()
+
+
+def make_sharded_vecenv(num_envs_total: int, **kwargs) -> VecEnv:
+    """This rank's shard (contiguous env ids) of a num_envs_total batch; one process per GPU."""
+    rank, world, local = env_rank()
+    start, end = shard_range(num_envs_total, world, rank)
+    kwargs.setdefault("device", local)
+    return VecEnv(end - start, env_offset=start, **kwargs)

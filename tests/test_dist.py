@@ -1,0 +1,110 @@
+"""Multi-GPU path on CPU: env sharding, the episode-statistics all-reduce over gloo
+(world_size 2), and sharded emulation == single-process emulation for the same env ids
+(host-simulation build of the HIP kernels on each rank)."""
+import hashlib
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from pokegym_amd.dist import STAT_FIELDS, EpisodeStats, shard_range
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def test_shard_range_partitions_contiguously():
+    for n in (1, 7, 64, 262144, 262145):
+        for w in (1, 2, 3, 8):
+            rs = [shard_range(n, w, r) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
+            sizes = [b - a for a, b in rs]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_episode_stats_accumulate():
+    st = EpisodeStats(3, "cpu")
+    r = torch.tensor([1.0, 2.0, 3.0], dtype=torch.float64)
+    st.update(r, torch.tensor([0, 0, 0], dtype=torch.uint8))
+    st.update(r, torch.tensor([1, 0, 0], dtype=torch.uint8))
+    st.update(r, torch.tensor([0, 1, 1], dtype=torch.uint8))
+    s = st.allreduce()
+    assert s["episodes"] == 3
+    assert s["episodic_return_sum"] == 2.0 + 6.0 + 9.0
+    assert s["episode_length_sum"] == 2 + 3 + 3
+    assert s["steps"] == 9 and s["reward_sum"] == 18.0
+    assert st.ep_return.tolist() == [1.0, 0.0, 0.0]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_dir, fn):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fn(rank, world, out_dir)
+    finally:
+        dist.destroy_process_group()
+
+
+def _stats_fn(rank, world, out_dir):
+    st = EpisodeStats(4, "cpu")
+    r = torch.full((4,), float(rank + 1), dtype=torch.float64)
+    st.update(r, torch.tensor([1, 0, 1, 0], dtype=torch.uint8))
+    s = st.allreduce()
+    with open(os.path.join(out_dir, f"stats{rank}.txt"), "w") as f:
+        f.write(repr([s[k] for k in STAT_FIELDS]))
+
+
+def test_stats_allreduce_gloo_world2(tmp_path):
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), _stats_fn), nprocs=2, join=True)
+    got = [eval(open(tmp_path / f"stats{r}.txt").read()) for r in range(2)]
+    # episodes: 2 per rank; returns: 2*1 + 2*2; lengths 4; reward sums 4*1 + 4*2; steps 8
+    assert got[0] == got[1] == [6.0, 4.0, 4.0, 12.0, 8.0]
+
+
+N_ENVS, STEPS = 6, 2
+
+
+def _actions():
+    return np.random.default_rng(3).integers(0, 8, (STEPS, N_ENVS)).astype(np.uint8)
+
+
+def _run_hostsim(env_ids, acts):
+    sys.path.insert(0, os.path.join(HERE, "hostsim"))
+    from sim import SimEmulator
+    from pokegym_amd.testrom.game import game_rom
+    emu = SimEmulator(game_rom(), len(env_ids), None, render=True)
+    for t in range(STEPS):
+        emu.step(acts[t, env_ids])
+    out = [hashlib.sha1(emu.snapshot(i)).hexdigest() for i in range(len(env_ids))]
+    emu.close()
+    return out
+
+
+def _shard_fn(rank, world, out_dir):
+    a, b = shard_range(N_ENVS, world, rank)
+    hashes = _run_hostsim(list(range(a, b)), _actions())
+    allh = [None] * world
+    dist.all_gather_object(allh, hashes)
+    if rank == 0:
+        with open(os.path.join(out_dir, "shards.txt"), "w") as f:
+            f.write(repr([h for part in allh for h in part]))
+
+
+@pytest.mark.slow
+def test_sharded_emulation_equals_single_process(tmp_path):
+    single = _run_hostsim(list(range(N_ENVS)), _actions())
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), _shard_fn), nprocs=2, join=True)
+    assert eval(open(tmp_path / "shards.txt").read()) == single

@@ -1,0 +1,39 @@
+"""Gymnasium/PufferLib surfaces on the MI355X (through the C ABI)."""
+import os
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+def test_environment_reset_step_shapes(tmp_path):
+    from pokegym_amd.env import Environment
+    from pokegym_amd.testrom.game import game_rom
+    rom = tmp_path / "pkbench.gb"
+    rom.write_bytes(game_rom())
+    env = Environment(rom_path=str(rom), max_episode_steps=3)
+    obs, info = env.reset()
+    assert obs.shape == (72, 80, 4) and obs.dtype == np.uint8 and info == {}
+    for t in range(3):
+        obs, rew, term, trunc, info = env.step(t % 8)
+        assert isinstance(rew, float) and term == trunc
+    assert term  # time >= max_episode_steps
+    assert env.observation_space.shape == (72, 80, 4) and env.action_space.n == 8
+    env.close()
+
+
+@pytest.mark.gpu
+def test_vecenv_steps_and_autoresets():
+    import torch
+    from pokegym_amd.env import VecEnv
+    from pokegym_amd.testrom.game import game_rom
+    env = VecEnv(128, rom=game_rom(), max_episode_steps=2, log_interval=4)
+    obs, _ = env.reset()
+    assert obs.shape == (128, 72, 80, 4) and obs.device.type == "cuda"
+    for t in range(4):
+        obs, rew, term, trunc, infos = env.step(torch.randint(0, 8, (128,), device=env.device))
+    assert term.all()
+    assert infos and infos[0]["episodes"] == 256
+    env.close()
