@@ -13,8 +13,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libpokegym_amd.so")
-SOURCES = ["pk_kernels.hip", "pk_reward.hip", "pk_capi.cpp"]
-HEADERS = ["pk_layout.h", "pk_decode.h", "pk_reward.h", "pk_reward_tables.h", os.path.join("..", "..", "include", "pokegym_amd.h")]
+SOURCES = ["pk_step.hip", "pk_kernels.hip", "pk_reward.hip", "pk_capi.cpp"]
+HEADERS = ["pk_layout.h", "pk_ucode.h", "pk_render.h", "pk_reward.h", "pk_reward_tables.h", os.path.join("..", "..", "include", "pokegym_amd.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PK_OFFLOAD_ARCH", "gfx950")
 

@@ -16,7 +16,7 @@
 #include <vector>
 
 #include "../../include/pokegym_amd.h"
-#include "pk_decode.h"
+#include "pk_ucode.h"
 #include "pk_layout.h"
 #include "pk_reward.h"
 
@@ -219,6 +219,7 @@ void export_v9(const Template& tp, const uint32_t* regs, const uint8_t* mem, con
 struct pk_handle {
     int device = 0;
     uint32_t n = 0, npad = 0, ngroups = 0;
+    uint32_t wave_lanes = 64;
     uint32_t frames = 24, release = 8, flags = 0, max_steps = 20480;
     uint32_t mbc = 3, bank_mask = 0;
     uint8_t* mem = nullptr;
@@ -226,8 +227,7 @@ struct pk_handle {
     uint32_t* lat = nullptr;
     uint8_t* screen = nullptr;
     uint8_t* rom = nullptr;
-    pk_rom_entry* rom16 = nullptr;
-    uint32_t* dtab = nullptr;
+    uint32_t* ucode = nullptr;  // microcode table (pk_ucode.h)
     uint8_t* t_mem = nullptr;
     uint32_t* t_regs = nullptr;
     uint32_t* t_lat = nullptr;
@@ -279,7 +279,7 @@ void pk_destroy(pk_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
-    void* ptrs[] = {h->mem, h->regs, h->lat, h->screen, h->rom, h->rom16, h->bank_slot, h->slot_bank, h->dtab, h->t_mem, h->t_regs,
+    void* ptrs[] = {h->mem, h->regs, h->lat, h->screen, h->rom, h->ucode, h->bank_slot, h->slot_bank, h->t_mem, h->t_regs,
                     h->t_lat, h->t_screen, h->scratch, h->rs, h->rsd, h->seen, h->mask, h->cutc, h->obs, h->reload};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -307,6 +307,11 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     h->n = cfg->n_envs;
     h->npad = (cfg->n_envs + PK_LANES - 1) / PK_LANES * PK_LANES;
     h->ngroups = h->npad / PK_LANES;
+    if (const char* wl = getenv("PK_WAVE_LANES")) {
+        int v = atoi(wl);
+        if (v != 64 && v != 32 && v != 16) return fail(-EINVAL, "PK_WAVE_LANES must be 64, 32 or 16");
+        h->wave_lanes = (uint32_t)v;
+    }
     h->frames = cfg->frame_skip;
     h->release = cfg->release_frame;
     h->flags = cfg->flags;
@@ -338,8 +343,7 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     ALLOC(h->lat, 3 * h->lat_stride * 4);
     ALLOC(h->screen, (size_t)h->npad * PK_SCREEN);
     ALLOC(h->rom, cfg->rom_len);
-    ALLOC(h->rom16, cfg->rom_len * sizeof(pk_rom_entry));
-    ALLOC(h->dtab, 1024 * 4);
+    ALLOC(h->ucode, PK_UC_ENTRIES * PK_UE_WORDS * 4);
     ALLOC(h->bank_slot, 128);
     ALLOC(h->slot_bank, PK_LDS_SLOTS);
     ALLOC(h->t_mem, PK_PHYS);
@@ -357,14 +361,11 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
         ALLOC(h->reload, h->npad);
     }
 #undef ALLOC
-    uint32_t dt[1024];
-    pk_build_dtab(dt);
-    std::vector<pk_rom_entry> rom16(cfg->rom_len);
-    pk_build_rom16(cfg->rom, (uint32_t)cfg->rom_len, dt, rom16.data());
+    std::vector<uint32_t> uc(PK_UC_ENTRIES * PK_UE_WORDS);
+    pk_build_ucode(uc.data());
     hipError_t e = hipSuccess;
-    if (e == hipSuccess) e = hipMemcpy(h->rom16, rom16.data(), rom16.size() * sizeof(pk_rom_entry), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->rom, cfg->rom, cfg->rom_len, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(h->dtab, dt, sizeof dt, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->ucode, uc.data(), uc.size() * 4, hipMemcpyHostToDevice);
     {
         // ROM banks staged in LDS by the step kernel: bank 0 and the first banks after it
         // (override the count with PK_LDS_SLOTS=1..6 for experiments)
@@ -472,12 +473,13 @@ int pk_step(pk_handle* h, const uint8_t* actions, uint8_t* screen_out, double* r
     HIPCHK(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
     PkStepArgs a;
-    a.mem = h->mem; a.rom = h->rom; a.rom16 = h->rom16; a.regs = h->regs; a.dtab = h->dtab; a.actions = actions;
+    a.mem = h->mem; a.rom = h->rom; a.regs = h->regs; a.ucode = h->ucode; a.actions = actions;
     a.lat = h->lat; a.screen = h->screen; a.n = h->n; a.npad = h->npad;
     a.rom_bank_mask = h->bank_mask; a.mbc = h->mbc; a.frames = h->frames;
     a.release_frame = h->release; a.render_last = (h->flags & PK_F_RENDER) ? 1 : 0;
     a.lat_stride = (uint32_t)h->lat_stride;
     a.nslots = h->nslots; a.bank_slot = h->bank_slot; a.slot_bank = h->slot_bank;
+    a.wave_lanes = h->wave_lanes;
     int rc;
     if (h->prof && (rc = prof_event(h, s))) return rc;
     HIPCHK(pk_launch_step(a, s));

@@ -1,0 +1,612 @@
+// pk_step.hip — K1, the MI355X (gfx950) env.step kernel: 24 emulated DMG frames per env-step, one
+// wavefront lane per emulator.  Replaces PyBoy's tick() loop as pokegym drives it in
+// pokegym/pyboy_binding.py:71-91 (run_action_on_emulator: press, 24 ticks, release before tick 8,
+// render only tick 24).  Semantics are pinned bit-exactly to the CPU oracle (oracle/gbcore.c,
+// a restatement of PyBoy 1.x): cpu_tick / cpu_check_interrupts, cpu_execute, bus_read/bus_write,
+// lcd_tick, timer_tick, the HALT fast-forward of gb_tick.
+//
+// SIMT design (one wave = 64 independent emulators that drift apart within a few frames):
+//   * every lane runs the SAME instruction sequence per emulated instruction: front-end
+//     (interrupts/HALT) -> fetch (LDS-staged ROM) -> microcode entry (LDS, pk_ucode.h) -> address
+//     -> read -> fused datapath -> register writeback (two v_perm_b32) -> write -> timer/LCD.
+//     Selections are written with sel() on precomputed values so the compiler emits v_cndmask,
+//     not divergent branch trees (the previous select-chain datapath compiled into ~600 SALU of
+//     exec-mask bookkeeping per emulated instruction).
+//   * only paths that a lane takes rarely (<1 % of iterations: special IO, MBC, OAM DMA, SRAM,
+//     deferred-line flush, frame end, DAA, timer overflow) are real branches.
+//   * ROM bank 0 + the hottest switchable banks and the microcode table live in LDS; the RAM
+//     images are lane-interleaved in HBM (pk_layout.h) so lanes at the same guest address coalesce.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pk_layout.h"
+#include "pk_render.h"
+#include "pk_ucode.h"
+
+#define FRAME_CYCLES 70224u
+#define CPU_IME 1u
+#define CPU_HALT 2u
+#define CPU_QUEUED 4u
+#define CPU_CRASH 8u
+
+// debug hooks: the host-simulation build (tests/hostsim) records an instruction trace and
+// per-iteration event bits; the gfx950 build compiles them away.
+#ifndef PK_TRACE
+#define PK_TRACE(env, pc, w0, w1, sp, op) ((void)0)
+#endif
+#ifndef PK_ITER
+#define PK_ITER(env, ev) ((void)(ev))
+#endif
+enum {
+    PK_EV_EXEC = 1u << 0, PK_EV_F_LDS = 1u << 1, PK_EV_F_ROM16 = 1u << 2, PK_EV_F_BUS = 1u << 3,
+    PK_EV_INT = 1u << 4, PK_EV_IDLE = 1u << 5, PK_EV_RD = 1u << 6, PK_EV_RD_ROMLDS = 1u << 7,
+    PK_EV_RD_ROMG = 1u << 8, PK_EV_RD_RAM = 1u << 9, PK_EV_RD_IO = 1u << 10, PK_EV_RD2 = 1u << 11,
+    PK_EV_WR = 1u << 12, PK_EV_WR_SLOW = 1u << 13, PK_EV_WR2 = 1u << 14, PK_EV_LCD = 1u << 15,
+    PK_EV_TIMER = 1u << 16, PK_EV_FRAME = 1u << 17, PK_EV_FLUSH = 1u << 18, PK_EV_HRAM = 1u << 19,
+    PK_EV_JUMP = 1u << 20, PK_EV_CB = 1u << 21, PK_EV_FAM0 = 1u << 22 /* 22..27: unused here */,
+    PK_EV_RD_WRAM = 1u << 28, PK_EV_WR_WRAM = 1u << 29, PK_EV_WR_VRAM = 1u << 30, PK_EV_WR_HI = 1u << 31
+};
+
+// ---------------------------------------------------------------------------------------------
+// branch-free helpers: arguments are evaluated unconditionally, so ?: on them is a v_cndmask
+__device__ __forceinline__ u32 sel(bool c, u32 a, u32 b) { return c ? a : b; }
+__device__ __forceinline__ u32 bit(u32 w, int pos) { return (w >> pos) & 1u; }
+__device__ __forceinline__ int sfield(u32 w, int pos, int bits) { return ((int)(w << (32 - pos - bits))) >> (32 - bits); }
+__device__ __forceinline__ u32 perm(u32 hi, u32 lo, u32 s) { return __builtin_amdgcn_perm(hi, lo, s); }
+
+// lane state (VGPRs for the whole launch).  Never select between two fields by reference: that
+// makes LLVM take field addresses and spill the struct to scratch.
+struct St {
+    u32 w0, w1, sp, pc;   // w0 = C|B<<8|E<<16|D<<24, w1 = L|H<<8|F<<16|A<<24 (kernel-internal order)
+    u32 cpu;              // ime | halted<<1 | queued<<2 | crashed<<3 | stopped<<4 | IE<<8 | IF<<16
+    u32 clock, target;    // lcd.clock, lcd.clock_target
+    u32 lcd0, lcd1, lcd2; // LCDC|STAT<<8|LY<<16|LYC<<24, SCY|SCX<<8|WY<<16|WX<<24, BGP|OBP0<<8|OBP1<<16|next_mode<<24
+    u32 tim0;             // (DIV stale) | TIMA<<8 | TMA<<16 | TAC<<24
+    u32 divacc;           // DIV<<8 | DIV_counter (mod 2^16)
+    u32 timac;            // TIMA_counter
+    u32 mbc;              // rombank | rambank<<8 | ram_enabled<<16 | memorymodel<<24
+    u32 misc;             // joypad directional | standard<<8 | (ly_window+1)<<16
+    u32 rb;               // LDS byte offset of the switchable ROM bank, 0xFFFFFFFF = not staged
+    u32 npend;            // latched, not yet rasterised lines
+    u32 render, blank, frame_done;
+};
+
+struct Ctx {
+    const PkStepArgs* A;
+    u8* g;                // lane-interleaved RAM image of this wave's group
+    u32 lane, env, gid;
+    const u8* lds_rom;
+    const int8_t* lds_slot;
+};
+
+__device__ __forceinline__ u32 ld_img(const Ctx& c, u32 phys) { return c.g[phys * PK_LANES + c.lane]; }
+__device__ __forceinline__ void st_img(const Ctx& c, u32 phys, u32 v) { c.g[phys * PK_LANES + c.lane] = (u8)v; }
+
+// fast RAM: VRAM, WRAM, echo, OAM/unusable, HRAM — plain bytes of the image with no side effects
+__device__ __forceinline__ bool fast_ram(u32 a) {
+    const bool reg = ((0xD0u >> (a >> 13)) & 1u) != 0u;  // regions 0x8000, 0xC000, 0xE000
+    const bool io = a >= 0xFF00u && (a < 0xFF80u || a == 0xFFFFu);
+    return reg && !io;
+}
+__device__ __forceinline__ u32 fast_phys(u32 a) {
+    const u32 p = (a & 0x1FFFu) + sel(a < 0xA000u, PK_P_VRAM, PK_P_WRAM);
+    return sel(a >= 0xFE00u, PK_P_OAM + (a & 0x1FFu), p);
+}
+
+__device__ __forceinline__ u32 rom_bank(const Ctx& c, const St& s, u32 a) {
+    return sel(a < 0x4000u, 0u, (s.mbc & 0xFFu) & c.A->rom_bank_mask);
+}
+__device__ __forceinline__ u32 rom_read(const Ctx& c, const St& s, u32 a) {
+    const u32 off = a & 0x3FFFu;
+    if (a < 0x4000u) return c.lds_rom[a];
+    if (s.rb != 0xFFFFFFFFu) return c.lds_rom[s.rb + off];
+    return c.A->rom[rom_bank(c, s, a) * 0x4000u + off];
+}
+__device__ __forceinline__ u32 slot_base(const Ctx& c, u32 bank) {
+    const int sl = c.lds_slot[bank & 127u];
+    return sl >= 0 ? (u32)sl * 0x4000u : 0xFFFFFFFFu;
+}
+
+// ---------------------------------------------------------------------------------------------
+// LCD helpers (pyboy lcd.py) — oracle: gbcore.c lcd_set_lcdc
+__device__ __forceinline__ void lcd_set_lcdc(St& s, u32 v) {
+    s.lcd0 = setb8(s.lcd0, 0, v);
+    if (!(v & 0x80u)) {
+        s.clock = 0;
+        s.target = FRAME_CYCLES;
+        s.lcd0 = (s.lcd0 & 0xFF0000FFu) | ((bfe8(s.lcd0, 8) & 0xFCu) << 8);  // set_mode(0), LY = 0
+        s.lcd2 = setb8(s.lcd2, 24, 2u);
+    }
+}
+
+// joypad (pyboy interaction.py) — oracle: gbcore.c gb_button / joy_pull
+__device__ __forceinline__ void key_event(St& s, u32 button, bool pressed) {
+    const u32 od = bfe8(s.misc, 0), os = bfe8(s.misc, 8);
+    u32 nd = od, ns = os;
+    const u32 b = 1u << (button & 3u);
+    if (button < 4u) nd = pressed ? (nd & ~b) : (nd | b);
+    else ns = pressed ? (ns & ~b) : (ns | b);
+    s.misc = (s.misc & 0xFFFF0000u) | nd | (ns << 8);
+    if (((od ^ nd) & od) || ((os ^ ns) & os)) s.cpu |= 0x10u << 16;
+}
+
+// IO register read (FF00-FF7F, FFFF) — oracle: gbcore.c bus_read
+__device__ __forceinline__ u32 io_read(const Ctx& c, const St& s, u32 a) {
+    if (a == 0xFFFFu) return bfe8(s.cpu, 8);
+    const u32 lo = a & 0xFFu;
+    u32 v = ld_img(c, PK_P_IO + lo);  // plain IO / FF4C-FF7F backing bytes
+    v = sel(lo >= 0x10u && lo < 0x40u, 0u, v);  // sound: not emulated
+    v = sel(lo == 0x04u, bfe8(s.divacc, 8), v);
+    v = sel(lo == 0x05u, bfe8(s.tim0, 8), v);
+    v = sel(lo == 0x06u, bfe8(s.tim0, 16), v);
+    v = sel(lo == 0x07u, bfe8(s.tim0, 24), v);
+    v = sel(lo == 0x0Fu, bfe8(s.cpu, 16), v);
+    // FF40-FF4B: LCDC STAT SCY SCX LY LYC DMA BGP OBP0 OBP1 WY WX
+    const u32 k = lo - 0x40u;
+    if (k < 12u) {
+        // per register: word (0 lcd0, 1 lcd1, 2 lcd2, 3 zero) << 2 | byte, 4 bits each
+        const uint64_t tab = 0x76A98C325410ull;
+        const u32 e = (u32)(tab >> (4u * k)) & 15u;
+        const u32 w = sel((e >> 2) == 0u, s.lcd0, sel((e >> 2) == 1u, s.lcd1, sel((e >> 2) == 2u, s.lcd2, 0u)));
+        v = bfe8(w, 8u * (e & 3u));
+    }
+    return v;
+}
+
+// generic bus read (pyboy mb.getitem) — any address, used off the fast paths
+__device__ __forceinline__ u32 bus_read_any(const Ctx& c, const St& s, u32 a) {
+    if (a < 0x8000u) return rom_read(c, s, a);
+    if ((a & 0xE000u) == 0xA000u) {  // cartridge SRAM
+        if (c.A->mbc == 0u || !bfe8(s.mbc, 16)) return 0xFFu;
+        return ld_img(c, PK_P_SRAM + (bfe8(s.mbc, 8) & 3u) * 0x2000u + (a - 0xA000u));
+    }
+    if (a >= 0xFF00u && (a < 0xFF80u || a == 0xFFFFu)) return io_read(c, s, a);
+    return ld_img(c, fast_phys(a));
+}
+
+// generic bus write (pyboy mb.setitem): MBC3 registers, SRAM, IO registers, OAM DMA, IE, and
+// plain RAM (with the deferred-line flush before VRAM/OAM changes)
+__device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v) {
+    const PkStepArgs& A = *c.A;
+    if (a < 0x8000u) {  // MBC3.setitem
+        if (A.mbc == 0u) return;
+        if (a < 0x2000u) {
+            s.mbc = setb8(s.mbc, 16, ((v & 0x0Fu) == 0x0Au) ? 1u : 0u);
+        } else if (a < 0x4000u) {
+            v &= 0x7Fu;
+            s.mbc = setb8(s.mbc, 0, v == 0u ? 1u : v);
+            s.rb = slot_base(c, (s.mbc & 0xFFu) & A.rom_bank_mask);
+        } else if (a < 0x6000u) {
+            s.mbc = setb8(s.mbc, 8, v);
+        }
+        return;
+    }
+    if ((a & 0xE000u) == 0xA000u) {
+        if (A.mbc != 0u && bfe8(s.mbc, 16)) st_img(c, PK_P_SRAM + (bfe8(s.mbc, 8) & 3u) * 0x2000u + (a - 0xA000u), v);
+        return;
+    }
+    if (a >= 0xFF00u && (a < 0xFF80u || a == 0xFFFFu)) {
+        switch (a) {
+            case 0xFF00: {  // joypad select: the register reads back the pulled lines
+                const u32 p14 = (v >> 4) & 1u, p15 = (v >> 5) & 1u;
+                u32 r = (v | 0xCFu) & 0xFFu;
+                if (p14 != p15) r &= (!p14) ? bfe8(s.misc, 0) : bfe8(s.misc, 8);
+                st_img(c, PK_P_IO, r);
+                break;
+            }
+            case 0xFF04: s.divacc = 0; s.timac = 0; break;
+            case 0xFF05: s.tim0 = setb8(s.tim0, 8, v); break;
+            case 0xFF06: s.tim0 = setb8(s.tim0, 16, v); break;
+            case 0xFF07: s.tim0 = setb8(s.tim0, 24, v & 7u); break;
+            case 0xFF0F: s.cpu = setb8(s.cpu, 16, v); break;
+            case 0xFF40: lcd_set_lcdc(s, v); break;
+            case 0xFF41: s.lcd0 = setb8(s.lcd0, 8, (bfe8(s.lcd0, 8) & 0x87u) | (v & 0x78u)); break;
+            case 0xFF42: s.lcd1 = setb8(s.lcd1, 0, v); break;
+            case 0xFF43: s.lcd1 = setb8(s.lcd1, 8, v); break;
+            case 0xFF44: break;  // LY is read-only
+            case 0xFF45: s.lcd0 = setb8(s.lcd0, 24, v); break;
+            case 0xFF46: {  // OAM DMA: instantaneous 160-byte copy (pyboy mb.transfer_DMA)
+                if (s.npend) {
+                    flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.env, c.gid);
+                    s.npend = 0;
+                }
+                const u32 src = v << 8;
+                for (u32 n = 0; n < 0xA0u; n++) st_img(c, PK_P_OAM + n, bus_read_any(c, s, (src + n) & 0xFFFFu));
+                break;
+            }
+            case 0xFF47: s.lcd2 = setb8(s.lcd2, 0, v); break;
+            case 0xFF48: s.lcd2 = setb8(s.lcd2, 8, v); break;
+            case 0xFF49: s.lcd2 = setb8(s.lcd2, 16, v); break;
+            case 0xFF4A: s.lcd1 = setb8(s.lcd1, 16, v); break;
+            case 0xFF4B: s.lcd1 = setb8(s.lcd1, 24, v); break;
+            case 0xFFFF: s.cpu = setb8(s.cpu, 8, v); break;
+            default:
+                if (a >= 0xFF10u && a < 0xFF40u) break;  // sound: not emulated
+                st_img(c, PK_P_IO + (a & 0xFFu), v);
+                break;
+        }
+        return;
+    }
+    if (s.npend && (a < 0xA000u || (a >= 0xFE00u && a < 0xFEA0u))) {
+        flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.env, c.gid);
+        s.npend = 0;
+    }
+    st_img(c, fast_phys(a), v);
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1
+__global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
+    __shared__ __attribute__((aligned(16))) u32 lds_uc[PK_UC_ENTRIES * PK_UE_WORDS];
+    __shared__ __attribute__((aligned(16))) u8 lds_rom[PK_LDS_SLOTS * 0x4000u];
+    __shared__ int8_t lds_slot[128];
+    for (u32 i = threadIdx.x; i < PK_UC_ENTRIES * PK_UE_WORDS; i += blockDim.x) lds_uc[i] = A.ucode[i];
+    for (u32 i = threadIdx.x; i < 128u; i += blockDim.x) lds_slot[i] = A.bank_slot[i];
+    for (u32 sl = 0; sl < A.nslots; sl++) {
+        const uint4* src = reinterpret_cast<const uint4*>(A.rom + (size_t)A.slot_bank[sl] * 0x4000u);
+        uint4* dst = reinterpret_cast<uint4*>(lds_rom + sl * 0x4000u);
+        for (u32 i = threadIdx.x; i < 0x4000u / 16u; i += blockDim.x) dst[i] = src[i];
+    }
+    __syncthreads();
+
+    // thread -> env: the first wave_lanes lanes of each wave carry envs (fewer envs per wave =
+    // more waves per SIMD for the same env count); the RAM layout is unchanged.
+    const u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const u32 wl = tid & (PK_LANES - 1u);
+    if (wl >= A.wave_lanes) return;
+    const u32 env = (tid >> 6) * A.wave_lanes + wl;
+    if (env >= A.npad) return;
+    Ctx c;
+    c.A = &A;
+    c.lane = env & (PK_LANES - 1u);
+    c.env = env;
+    c.gid = __builtin_amdgcn_readfirstlane(env / PK_LANES);
+    c.g = A.mem + (size_t)c.gid * PK_GROUP_STRIDE;
+    c.lds_rom = lds_rom;
+    c.lds_slot = lds_slot;
+
+    const u32 np = A.npad;
+    u32* R = A.regs;
+    St s;
+    s.w0 = R[PK_R_W0 * np + env];
+    s.w1 = perm(R[PK_R_W1 * np + env], R[PK_R_W1 * np + env], 0x02030100u);  // L H A F -> L H F A
+    s.sp = R[PK_R_SP * np + env];
+    s.pc = R[PK_R_PC * np + env];
+    s.cpu = R[PK_R_CPU * np + env];
+    s.clock = R[PK_R_CLOCK * np + env];
+    s.target = R[PK_R_TARGET * np + env];
+    s.lcd0 = R[PK_R_LCD0 * np + env];
+    s.lcd1 = R[PK_R_LCD1 * np + env];
+    s.lcd2 = R[PK_R_LCD2 * np + env];
+    {
+        const u32 t0 = R[PK_R_TIM0 * np + env], t1 = R[PK_R_TIM1 * np + env];
+        s.tim0 = t0;
+        s.divacc = ((t0 & 0xFFu) << 8) | (t1 & 0xFFu);
+        s.timac = t1 >> 16;
+    }
+    s.mbc = R[PK_R_MBC * np + env];
+    s.misc = R[PK_R_MISC * np + env];
+    s.rb = slot_base(c, (s.mbc & 0xFFu) & A.rom_bank_mask);
+    s.npend = 0;
+    s.blank = 0;
+    s.frame_done = 0;
+    u32 icount = 0;
+
+    const bool active = env < A.n;
+    u32 frame = active ? 0u : A.frames;
+    const u32 action = active ? A.actions[env] : 8u;
+    // pyboy_binding.py:7-40 ACTIONS: Down Left Right Up A B Start Select -> interaction buttons
+    // (0 Right 1 Left 2 Up 3 Down 4 A 5 B 6 Select 7 Start); 8+ = no button (extension)
+    const u32 btn = action == 0u ? 3u : action == 1u ? 1u : action == 2u ? 0u : action == 3u ? 2u
+                  : action == 4u ? 4u : action == 5u ? 5u : action == 6u ? 7u : action == 7u ? 6u : 0xFFu;
+    if (active && btn != 0xFFu) key_event(s, btn, true);
+    if (active && A.frames > 0u && A.release_frame == 0u && btn != 0xFFu) key_event(s, btn, false);
+    s.render = (A.render_last && frame + 1u == A.frames) ? 1u : 0u;
+    if (s.render) {
+        u32* lat2 = A.lat + 2u * A.lat_stride;
+        for (u32 y = 0; y < PK_ROWS; y++) lat2[(c.gid * PK_ROWS + y) * PK_LANES + c.lane] &= ~0x100u;
+    }
+    const uint4* ucv = reinterpret_cast<const uint4*>(lds_uc);
+    const u32* romw = reinterpret_cast<const u32*>(lds_rom);
+
+    u32 budget = 0;  // frame watchdog (oracle/gbcore.c PK_FRAME_BUDGET)
+    while (frame < A.frames) {
+        u32 ev = 0;
+        // ---------------- front-end: cpu.tick / check_interrupts ----------------
+        const u32 cpu0 = s.cpu;
+        const u32 pend = (cpu0 >> 8) & (cpu0 >> 16) & 0x1Fu;
+        const bool crashed = (cpu0 & CPU_CRASH) != 0u;
+        const bool halted = (cpu0 & CPU_HALT) != 0u;
+        const bool queued = (cpu0 & CPU_QUEUED) != 0u;
+        const bool doint = !crashed && !queued && pend != 0u;
+        const bool dispatch = doint && (cpu0 & CPU_IME) != 0u;
+        const bool wake = !crashed && !doint && halted && queued;
+        const bool exec = !crashed && !doint && (!halted || queued);
+        const u32 pc = (s.pc + sel((doint && halted) || wake, 1u, 0u)) & 0xFFFFu;
+        const u32 intflag = pend & (0u - pend);
+        s.cpu = sel(doint, (cpu0 | CPU_QUEUED) & ~CPU_HALT, sel(wake, cpu0 & ~CPU_HALT, cpu0)) ^ sel(dispatch, intflag << 16, 0u);
+        u32 di = sel(dispatch, PK_UC_INT, sel(doint, PK_UC_NOP0, PK_UC_IDLE));
+        u32 bytes = (0x40u + 8u * (u32)__builtin_ctz(intflag | 0x20u)) << 8;  // INT: vector as imm16
+
+        // ---------------- fetch: LDS-staged ROM, else the RAM image / generic bus ----------------
+        if (exec) {
+            const u32 off = pc & 0x3FFFu;
+            if (pc < 0x8000u && (pc < 0x4000u || s.rb != 0xFFFFFFFFu) && off < 0x3FFEu) {
+                const u32 la = sel(pc < 0x4000u, pc, s.rb + off);
+                bytes = __builtin_amdgcn_alignbyte(romw[(la >> 2) + 1u], romw[la >> 2], la & 3u);
+                ev |= PK_EV_F_LDS;
+            } else if (fast_ram(pc) && fast_ram((pc + 2u) & 0xFFFFu) && ((pc ^ (pc + 2u)) & 0xFE00u) == 0u) {
+                const u32 p = fast_phys(pc);  // code in RAM (e.g. the HRAM OAM-DMA wait loop)
+                bytes = ld_img(c, p) | (ld_img(c, p + 1u) << 8) | (ld_img(c, p + 2u) << 16);
+                ev |= PK_EV_F_BUS | sel(pc >= 0xFF80u, PK_EV_HRAM, 0u);
+            } else {
+                bytes = bus_read_any(c, s, pc) | (bus_read_any(c, s, (pc + 1u) & 0xFFFFu) << 8)
+                      | (bus_read_any(c, s, (pc + 2u) & 0xFFFFu) << 16);
+                ev |= sel(pc < 0x8000u, PK_EV_F_ROM16, PK_EV_F_BUS);
+            }
+            const u32 op = bytes & 0xFFu;
+            di = sel(op == 0xCBu, 256u + ((bytes >> 8) & 0xFFu), op);
+            icount += 1u;
+            ev |= PK_EV_EXEC | sel(op == 0xCBu, PK_EV_CB, 0u);
+            PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, op);
+        }
+        if (dispatch) ev |= PK_EV_INT;
+        if (!exec && !dispatch) ev |= PK_EV_IDLE;
+        const uint4 e0 = ucv[di * 2u], e1 = ucv[di * 2u + 1u];
+        const u32 D = e0.x, U = e0.y, PX = e0.z, PY = e0.w, S0 = e1.x, S1 = e1.y, PA = e1.z, K = e1.w;
+
+        // ---------------- operands, condition, memory address ----------------
+        const u32 w0 = s.w0, w1 = s.w1, sp = s.sp;
+        const u32 b1 = (bytes >> 8) & 0xFFu;
+        const u32 imm16 = (bytes >> 8) & 0xFFFFu;
+        const u32 F = (w1 >> 16) & 0xFFu;
+        const u32 fc = (F >> 4) & 1u;
+        const u32 hl = w1 & 0xFFFFu;
+        const u32 pcn = (pc + (D & 3u)) & 0xFFFFu;
+        const u32 taken = (((F | 0x100u) >> ((D >> PK_DB_CPOS) & 15u)) & 1u) ^ bit(D, PK_DB_CINV);
+        const u32 abase = perm(w1, w0, PA);
+        const u32 aim = sel(bit(D, PK_DB_AHN), 0xFF00u | b1, imm16);
+        const u32 asrc = sel(bit(D, PK_DB_ASP), sp, sel(bit(D, PK_DB_AIMM), aim, abase));
+        const u32 addr0 = (asrc + (u32)sfield(D, PK_DB_AOFF, 2)) & 0xFFFFu;
+        const u32 addr1 = (addr0 + (u32)sfield(D, PK_DB_ADIR, 2)) & 0xFFFFu;
+
+        // ---------------- memory reads (m0 at addr0, m1 at addr1) ----------------
+        u32 m0 = 0, m1 = 0;
+        const bool rd2 = bit(D, PK_DB_RD2) != 0u;
+        if (bit(D, PK_DB_RD)) {
+            const bool f0 = fast_ram(addr0), f1 = !rd2 || fast_ram(addr1);
+            if (f0 && f1) {
+                m0 = ld_img(c, fast_phys(addr0));
+                if (rd2) m1 = ld_img(c, fast_phys(addr1));
+                ev |= PK_EV_RD_RAM;
+            } else if (addr0 < 0x8000u && (!rd2 || addr1 < 0x8000u)) {
+                m0 = rom_read(c, s, addr0);
+                if (rd2) m1 = rom_read(c, s, addr1);
+                ev |= PK_EV_RD_ROMLDS;
+            } else {
+                m0 = bus_read_any(c, s, addr0);
+                if (rd2) m1 = bus_read_any(c, s, addr1);
+                ev |= PK_EV_RD_IO;
+            }
+            ev |= PK_EV_RD | sel(rd2, PK_EV_RD2, 0u) | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
+                | sel(addr0 >= 0xC000u && addr0 < 0xFE00u, PK_EV_RD_WRAM, 0u);
+        }
+        const u32 m16 = m0 | (m1 << 8);
+
+        // ---------------- fused datapath ----------------
+        const u32 X = sel(bit(U, PK_UB_XSP), sp, sel(bit(U, PK_UB_XMEM), m0, perm(w1, w0, PX)));
+        const u32 sx8 = (u32)(int)(int8_t)(u8)b1 & 0xFFFFu;
+        const u32 imm = sel(bit(U, PK_UB_SEXT), sx8, sel(bit(U, PK_UB_IMM8), b1, imm16));
+        const u32 Y = sel(bit(U, PK_UB_YIMM), imm, sel(bit(U, PK_UB_YMEM), m16, sel(bit(D, PK_DB_YSP), sp, perm(w1, w0, PY))))
+                    | (K & 0xFFu);
+        // adder: r = X + (sub ? ~Y : Y) + cin; carries into each bit = X ^ Y' ^ r
+        const u32 sub = bit(U, PK_UB_SUB);
+        const u32 Yx = Y ^ ((0u - sub) & 0xFFFFu);
+        const u32 r = X + Yx + (sub ^ (bit(U, PK_UB_USEC) & fc));
+        const u32 cv = X ^ Yx ^ r;
+        const u32 hsh = 4u + 8u * bit(U, PK_UB_HC16);
+        const u32 hf = ((cv >> hsh) & 1u) ^ sub;
+        const u32 cf = ((cv >> (hsh + 4u)) & 1u) ^ sub;
+        // logic
+        const u32 lop = (U >> PK_UB_LOP) & 3u;
+        const u32 lres = sel(lop == 0u, X & Y, sel(lop == 1u, X ^ Y, X | Y));
+        // rotate / shift / swap
+        const u32 x8 = X & 0xFFu;
+        const bool rdir = bit(U, PK_UB_RDIR) != 0u;
+        const u32 b7 = x8 >> 7, rob = sel(rdir, x8 & 1u, b7);
+        const u32 rbin = (U >> PK_UB_RBIN) & 3u;
+        const u32 bin = sel(rbin == 1u, fc, sel(rbin == 2u, rob, sel(rbin == 3u, b7, 0u)));
+        const u32 rsh = sel(rdir, (x8 >> 1) | (bin << 7), ((x8 << 1) | bin) & 0xFFu);
+        const u32 rot = sel(bit(U, PK_UB_SWAP), ((x8 >> 4) | (x8 << 4)) & 0xFFu, rsh);
+        // results
+        const u32 r8s = (U >> PK_UB_R8) & 3u;
+        u32 res8 = sel(r8s == 0u, Y, sel(r8s == 1u, r, sel(r8s == 2u, lres, rot))) & 0xFFu;
+        const u32 hl1 = (hl + (u32)sfield(U, PK_UB_HLINC, 2)) & 0xFFFFu;
+        const u32 res16 = sel(bit(U, PK_UB_R16HL), hl1, r & 0xFFFFu);
+        // flags: F' = (F & keep) | const | Z | H | C
+        const u32 fcs = (U >> PK_UB_FC) & 3u;
+        const u32 cbit = sel(fcs == 1u, cf, sel(fcs == 2u, rob, sel(fcs == 3u, fc ^ 1u, 0u)));
+        u32 nf = (F & (K >> PK_KB_FKEEP)) | (K >> PK_KB_FCONST) | sel(bit(U, PK_UB_FZ) && res8 == 0u, 0x80u, 0u)
+               | ((bit(U, PK_UB_FH) & hf) << 5) | (cbit << 4);
+        nf = sel(bit(U, PK_UB_FPOP), m0 & 0xF0u, nf) & 0xFFu;
+        if (bit(D, PK_DB_DAA)) {  // DAA (opcodes.py DAA_27), rare
+            const u32 a = w1 >> 24;
+            u32 corr = ((F & 0x20u) ? 0x06u : 0u) | ((F & 0x10u) ? 0x60u : 0u);
+            if (!(F & 0x40u)) corr |= ((a & 0x0Fu) > 0x09u ? 0x06u : 0u) | (a > 0x99u ? 0x60u : 0u);
+            res8 = ((F & 0x40u) ? (a - corr) : (a + corr)) & 0xFFu;
+            nf = (F & 0x40u) | (res8 == 0u ? 0x80u : 0u) | ((corr & 0x60u) ? 0x10u : 0u);
+        }
+        // register writeback: val = res16 | F' << 16 | res8 << 24 through the per-op byte selectors
+        const u32 val = res16 | (nf << 16) | (res8 << 24);
+        s.w0 = perm(val, w0, S0);
+        s.w1 = perm(val, w1, S1);
+
+        // ---------------- control transfer, SP, IME/HALT ----------------
+        const u32 tsrc = (D >> PK_DB_TSRC) & 7u;
+        const u32 jrt = (pc + 2u + sx8) & 0xFFFFu;
+        const u32 tgt = sel(tsrc == PK_T_IMM, imm16, sel(tsrc == PK_T_HL, hl, sel(tsrc == PK_T_JR, jrt, sel(tsrc == PK_T_M16, m16, bytes & 0x38u))));
+        const bool jump = tsrc != 0u && taken != 0u;
+        s.pc = sel(jump, tgt, pcn);
+        if (jump) ev |= PK_EV_JUMP;
+        u32 cycles = ((D >> PK_DB_CYC) & 7u) * 4u + sel(taken != 0u, ((D >> PK_DB_XCYC) & 3u) * 4u, 0u);
+        const u32 sp2 = (sp + ((u32)sfield(U, PK_UB_SPD, 3) & (0u - taken))) & 0xFFFFu;
+        s.sp = sel(bit(U, PK_UB_SPW), res16, sp2);
+        {
+            const u32 ime = (D >> PK_DB_IME) & 3u;
+            u32 cpu = s.cpu;
+            cpu = sel(ime == 1u, cpu & ~CPU_IME, sel(ime == 2u, cpu | CPU_IME, cpu));
+            cpu |= (bit(D, PK_DB_HALT) * CPU_HALT) | (bit(D, PK_DB_CRASH) * (CPU_CRASH | CPU_HALT));
+            s.cpu = sel(exec, cpu & ~CPU_QUEUED, cpu);
+        }
+
+        // ---------------- memory writes (wv0 at addr0, wv1 at addr1) ----------------
+        if (bit(D, PK_DB_WR) && taken) {
+            const bool wr2 = bit(D, PK_DB_WR2) != 0u;
+            const u32 pushv = sel(bit(U, PK_UB_WPC), pcn, sel(bit(U, PK_UB_WSP), sp, Y & 0xFFFFu));
+            const u32 wv = sel(bit(U, PK_UB_W16), pushv, res8);
+            const bool hifirst = bit(D, PK_DB_ADIR + 1) != 0u;  // adir = -1: push writes the high byte first
+            const u32 wv0 = sel(hifirst, wv >> 8, wv) & 0xFFu, wv1 = sel(hifirst, wv, wv >> 8) & 0xFFu;
+            const bool f0 = fast_ram(addr0), f1 = !wr2 || fast_ram(addr1);
+            ev |= PK_EV_WR | sel(wr2, PK_EV_WR2, 0u) | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
+                | sel(addr0 >= 0xC000u && addr0 < 0xFE00u, PK_EV_WR_WRAM, sel(addr0 >= 0x8000u && addr0 < 0xA000u, PK_EV_WR_VRAM, 0u));
+            if (f0 && f1) {
+                if (s.npend) {
+                    const bool vo0 = addr0 < 0xA000u || (addr0 >= 0xFE00u && addr0 < 0xFEA0u);
+                    const bool vo1 = wr2 && (addr1 < 0xA000u || (addr1 >= 0xFE00u && addr1 < 0xFEA0u));
+                    if (vo0 || vo1) {
+                        flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, env, c.gid);
+                        s.npend = 0;
+                        ev |= PK_EV_FLUSH;
+                    }
+                }
+                st_img(c, fast_phys(addr0), wv0);
+                if (wr2) st_img(c, fast_phys(addr1), wv1);
+            } else {
+                bus_write_any(c, s, addr0, wv0);
+                if (wr2) bus_write_any(c, s, addr1, wv1);
+                ev |= PK_EV_WR_SLOW;
+            }
+        }
+
+        // ---------------- HALT fast-forward, timer, LCD (pyboy mb.tick) ----------------
+        if (s.cpu & CPU_HALT) {
+            const u32 tac = s.tim0 >> 24;
+            const u32 dsh = sel((tac & 3u) == 0u, 10u, sel((tac & 3u) == 1u, 4u, sel((tac & 3u) == 2u, 6u, 8u)));
+            const int tb = (tac & 4u) ? (int)((0x100u - bfe8(s.tim0, 8)) << dsh) - (int)s.timac : (1 << 16);
+            const int ta = (int)s.target - (int)s.clock;
+            const int mm = ta < tb ? ta : tb;
+            cycles = mm < 0 ? 0u : (u32)mm;
+        }
+        u32 irq = 0;
+        s.divacc = (s.divacc + cycles) & 0xFFFFu;
+        if (s.tim0 & 0x04000000u) {  // TAC enabled (timer.py Timer.tick)
+            const u32 tac = s.tim0 >> 24;
+            const u32 dsh = sel((tac & 3u) == 0u, 10u, sel((tac & 3u) == 1u, 4u, sel((tac & 3u) == 2u, 6u, 8u)));
+            u32 timac = s.timac + cycles;
+            u32 tima = bfe8(s.tim0, 8);
+            if (timac >= (1u << dsh)) {
+                const u32 mul = timac >> dsh;
+                timac -= mul << dsh;
+                tima += mul;
+                if (tima > 0xFFu) {
+                    tima = (tima - 0x100u + bfe8(s.tim0, 16)) & 0xFFu;
+                    irq |= 4u;
+                    ev |= PK_EV_TIMER;
+                }
+            }
+            s.tim0 = setb8(s.tim0, 8, tima);
+            s.timac = timac;
+        }
+        s.clock += cycles;
+        const u32 lcdc = s.lcd0 & 0xFFu;
+        if (lcdc & 0x80u) {
+            if (s.clock >= s.target) {  // lcd.tick mode transition
+                ev |= PK_EV_LCD;
+                const u32 nm = s.lcd2 >> 24;
+                u32 stat = bfe8(s.lcd0, 8), ly = bfe8(s.lcd0, 16);
+                const u32 lyc = s.lcd0 >> 24;
+                const bool changed = (stat & 3u) != nm;
+                stat = (stat & 0xFCu) | nm;
+                irq |= sel(changed && nm != 3u && ((stat >> (nm + 3u)) & 1u), 2u, 0u);
+                const bool m2 = nm == 2u, m3 = nm == 3u, m0 = nm == 0u, m1 = nm == 1u;
+                const bool wrap = m2 && ly == 153u;
+                if (wrap) {
+                    s.clock %= FRAME_CYCLES;
+                    s.target %= FRAME_CYCLES;
+                }
+                ly = sel(wrap, 0u, sel(m2 || m1, ly + 1u, ly));
+                s.target += sel(m2, 80u, sel(m3, 170u, sel(m0, 206u, 456u)));
+                const bool eq = lyc == ly, upd = m2 || m1;
+                stat = sel(upd, sel(eq, stat | 4u, stat & 0xFBu), stat);
+                irq |= sel(upd && eq && (stat & 0x40u), 2u, 0u);
+                const u32 nnext = sel(m2, 3u, sel(m3, 0u, sel(m0, sel(ly < 143u, 2u, 1u), sel(ly == 153u, 2u, 1u))));
+                const bool vbl = m1 && ly == 144u;
+                irq |= sel(vbl, 1u, 0u);
+                s.frame_done |= sel(vbl, 1u, 0u);
+                s.lcd0 = (s.lcd0 & 0xFF0000FFu) | (stat << 8) | (ly << 16);
+                s.lcd2 = (s.lcd2 & 0x00FFFFFFu) | (nnext << 24);
+                if (m0 && s.render && ly < PK_ROWS) {
+                    // latch this scanline's registers; rasterised by K2 (or flush_lines)
+                    const u32 wy = bfe8(s.lcd1, 16), wx = bfe8(s.lcd1, 24);
+                    int lw = (int)bfe8(s.misc, 16) - 1;
+                    if ((lcdc & 0x20u) && wy <= ly && (int)wx - 7 < (int)PK_COLS) lw += 1;
+                    const u32 idx = (c.gid * PK_ROWS + ly) * PK_LANES + c.lane;
+                    A.lat[idx] = lcdc | (bfe8(s.lcd1, 8) << 8) | (bfe8(s.lcd1, 0) << 16) | (wx << 24);
+                    A.lat[A.lat_stride + idx] = wy | ((s.lcd2 & 0xFFFFFFu) << 8);
+                    A.lat[2u * A.lat_stride + idx] = (u32)(lw + 1) | 0x100u;
+                    if (ly == PK_ROWS - 1u) lw = -1;
+                    s.misc = setb8(s.misc, 16, (u32)(lw + 1));
+                    s.npend += 1u;
+                }
+            }
+        } else if (s.clock >= FRAME_CYCLES) {
+            s.frame_done = 1u;
+            s.clock %= FRAME_CYCLES;
+            if (s.render) s.blank = 1u;
+        }
+        s.cpu |= irq << 16;
+        budget += cycles + 1u;
+        if (budget > 16u * FRAME_CYCLES) s.frame_done = 1u;
+        if (s.frame_done) ev |= PK_EV_FRAME;
+        PK_ITER(env, ev);
+        if (s.frame_done) {
+            s.frame_done = 0;
+            budget = 0;
+            frame += 1u;
+            if (frame == A.release_frame && btn != 0xFFu) key_event(s, btn, false);
+            s.render = (A.render_last && frame + 1u == A.frames) ? 1u : 0u;
+            if (s.render) {
+                u32* lat2 = A.lat + 2u * A.lat_stride;
+                for (u32 y = 0; y < PK_ROWS; y++) lat2[(c.gid * PK_ROWS + y) * PK_LANES + c.lane] &= ~0x100u;
+            }
+        }
+    }
+
+    if (!active) return;
+    R[PK_R_W0 * np + env] = s.w0;
+    R[PK_R_W1 * np + env] = perm(s.w1, s.w1, 0x02030100u);
+    R[PK_R_SP * np + env] = s.sp;
+    R[PK_R_PC * np + env] = s.pc;
+    R[PK_R_CPU * np + env] = s.cpu;
+    R[PK_R_CLOCK * np + env] = s.clock;
+    R[PK_R_TARGET * np + env] = s.target;
+    R[PK_R_LCD0 * np + env] = s.lcd0;
+    R[PK_R_LCD1 * np + env] = s.lcd1;
+    R[PK_R_LCD2 * np + env] = s.lcd2;
+    R[PK_R_TIM0 * np + env] = (s.tim0 & 0xFFFFFF00u) | ((s.divacc >> 8) & 0xFFu);
+    R[PK_R_TIM1 * np + env] = (s.divacc & 0xFFu) | (s.timac << 16);
+    R[PK_R_MBC * np + env] = s.mbc;
+    R[PK_R_MISC * np + env] = s.misc;
+    R[PK_R_TIME * np + env] += 1u;
+    R[PK_R_ICOUNT * np + env] = icount;
+    R[PK_R_RFLAGS * np + env] = s.blank | (s.npend << 8);
+}
+
+hipError_t pk_launch_step(const PkStepArgs& a, hipStream_t s) {
+    const u32 wl = a.wave_lanes;
+    const u32 block = wl >= 64u ? 256u : 512u;
+    const u32 threads = a.npad * (PK_LANES / wl);
+    const u32 grid = (threads + block - 1) / block;
+    hipLaunchKernelGGL(pk_step_kernel, dim3(grid), dim3(block), 0, s, a);
+    return hipGetLastError();
+}

@@ -1,0 +1,420 @@
+// pk_ucode.h — SM83 microcode for the K1 step kernel (pk_step.hip), built on the host and staged
+// in LDS.  One 32-byte entry per opcode (256 base + 256 CB-prefixed + 3 pseudo-ops) drives ONE
+// fused datapath that every lane runs each iteration, whatever opcode it holds:
+//
+//   X = SP | m0 | perm(w1:w0, PX)          Y = (imm | m16 | SP | perm(w1:w0, PY)) | yconst
+//   adder  r = X + (sub ? ~Y : Y) + cin;   carries = X ^ Y' ^ r  ->  H, C at bit 4/8 or 12/16
+//   logic  X & Y | X ^ Y | X | Y           rotate/shift unit on X
+//   val    = res16 | F' << 16 | res8 << 24;  w0 = perm(val, w0, S0);  w1 = perm(val, w1, S1)
+//
+// so an 8-bit write, a 16-bit pair write, the flags, POP AF and (HL+)/(HL-) are all the same two
+// v_perm_b32.  Register layout inside the kernel: w0 = C|B<<8|E<<16|D<<24,
+// w1 = L|H<<8|F<<16|A<<24 (bytes 0..7 of the perm source pair w1:w0: C B E D L H F A).
+//
+// Instruction semantics and cycle counts are those of PyBoy 1.x's generated opcodes.py as the
+// oracle restates them (oracle/gbcore.c cpu_execute / exec_cb / cpu_check_interrupts).
+#pragma once
+#include <stdint.h>
+
+// ---- entry layout: 8 dwords ----
+enum { PK_UE_D = 0, PK_UE_U, PK_UE_PX, PK_UE_PY, PK_UE_S0, PK_UE_S1, PK_UE_PA, PK_UE_K, PK_UE_WORDS };
+#define PK_UC_ENTRIES 515u
+#define PK_UC_INT 512u    // pseudo-op: interrupt dispatch (push PC, jump to the vector)
+#define PK_UC_IDLE 513u   // pseudo-op: halted / crashed CPU, 4 cycles
+#define PK_UC_NOP0 514u   // pseudo-op: interrupt pending with IME off (queued), 0 cycles
+
+// D word: memory, timing, control
+#define PK_DB_LEN 0       // 2 bits  instruction length
+#define PK_DB_RD 2        // read m0 at addr0
+#define PK_DB_RD2 3       // read m1 at addr1
+#define PK_DB_WR 4        // write wv0 at addr0
+#define PK_DB_WR2 5       // write wv1 at addr1
+#define PK_DB_ASP 6       // address source SP
+#define PK_DB_AIMM 7      // address source immediate
+#define PK_DB_AHN 8       // immediate address is 0xFF00|n
+#define PK_DB_AOFF 9      // 2 bits signed: addr0 = src + aoff
+#define PK_DB_ADIR 11     // 2 bits signed: addr1 = addr0 + adir
+#define PK_DB_CYC 13      // 3 bits cycles/4
+#define PK_DB_XCYC 16     // 2 bits extra cycles/4 when the condition holds
+#define PK_DB_CPOS 18     // 4 bits: condition = bit cpos of (F | 0x100)
+#define PK_DB_CINV 22     //         ^ cinv
+#define PK_DB_TSRC 23     // 3 bits jump target: 0 none 1 imm16 2 HL 3 JR 4 m16 5 RST
+#define PK_DB_IME 26      // 2 bits: 0 keep 1 clear 2 set
+#define PK_DB_HALT 28     // set HALT
+#define PK_DB_CRASH 29    // set CRASH|HALT (illegal opcode)
+#define PK_DB_DAA 30      // DAA (rare path)
+#define PK_DB_YSP 31      // Y = SP
+enum { PK_T_NONE = 0, PK_T_IMM, PK_T_HL, PK_T_JR, PK_T_M16, PK_T_RST };
+
+// U word: datapath
+#define PK_UB_XSP 0       // X = SP
+#define PK_UB_XMEM 1      // X = m0
+#define PK_UB_YIMM 2      // Y = immediate
+#define PK_UB_IMM8 3      // immediate = n (else nn)
+#define PK_UB_SEXT 4      // immediate = sign-extended n (16-bit)
+#define PK_UB_YMEM 5      // Y = m16
+#define PK_UB_SUB 6       // adder subtracts
+#define PK_UB_USEC 7      // adder carry-in from F.C (ADC/SBC)
+#define PK_UB_HC16 8      // H/C from bits 12/16 (else 4/8)
+#define PK_UB_R8 9        // 2 bits result8: 0 Y 1 adder 2 logic 3 rotate
+#define PK_UB_LOP 11      // 2 bits logic: 0 AND 1 XOR 2 OR
+#define PK_UB_RDIR 13     // rotate right (else left)
+#define PK_UB_RBIN 14     // 2 bits rotate-in bit: 0 zero 1 F.C 2 rotated-out bit 3 bit 7 (SRA)
+#define PK_UB_SWAP 16     // SWAP
+#define PK_UB_FZ 17       // Z from result8
+#define PK_UB_FH 18       // H from adder
+#define PK_UB_FC 19       // 2 bits C: 0 none 1 adder 2 rotate 3 !F.C
+#define PK_UB_FPOP 21     // F = m0 & 0xF0 (POP AF)
+#define PK_UB_HLINC 22    // 2 bits signed HL increment for (HL+)/(HL-)
+#define PK_UB_R16HL 24    // res16 = HL +- 1 (else adder)
+#define PK_UB_SPW 25      // SP = res16
+#define PK_UB_SPD 26      // 3 bits signed SP delta (PUSH/POP family), applied when the condition holds
+#define PK_UB_W16 29      // write value is 16-bit (else result8)
+#define PK_UB_WPC 30      // 16-bit write value = return PC
+#define PK_UB_WSP 31      // 16-bit write value = SP
+
+// K word: constants
+#define PK_KB_YCONST 0    // 8 bits ORed into Y
+#define PK_KB_FKEEP 8     // 8 bits: F bits kept
+#define PK_KB_FCONST 16   // 8 bits: F bits set
+
+// perm selectors over (w1:w0) = bytes C B E D L H F A ; 0x0C = 0x00, 0x0D = 0xFF
+#define PK_PZERO 0x0C0C0C0Cu
+
+static inline uint32_t pk_r8_byte(int r) {  // SM83 r8 index (B C D E H L (HL) A) -> byte in w1:w0
+    static const uint8_t b[8] = {1, 0, 3, 2, 5, 4, 0xFF, 7};
+    return b[r & 7];
+}
+static inline uint32_t pk_sel8(int r) { return 0x0C0C0C00u | pk_r8_byte(r); }
+static inline uint32_t pk_sel16(int p) {  // BC DE HL AF -> 16-bit (lo | hi<<8)
+    static const uint32_t s[4] = {0x0C0C0100u, 0x0C0C0302u, 0x0C0C0504u, 0x0C0C0706u};
+    return s[p & 3];
+}
+
+struct PkUop {
+    uint32_t d, u, px, py, s0, s1, pa, k;
+};
+
+// writeback selectors: identity, F always from val byte 2 (F' = kept bits | computed bits)
+#define PK_S0_ID 0x03020100u
+#define PK_S1_ID 0x03060100u
+static inline void pk_wb_r8(PkUop& o, int r) {  // dest r8 <- val byte 3 (result8)
+    uint32_t b = pk_r8_byte(r);
+    if (b < 4) o.s0 = (o.s0 & ~(0xFFu << (8 * b))) | (0x07u << (8 * b));
+    else o.s1 = (o.s1 & ~(0xFFu << (8 * (b - 4)))) | (0x07u << (8 * (b - 4)));
+}
+static inline void pk_wb_r16(PkUop& o, int p) {  // dest pair BC DE HL <- val bytes 0,1 (res16)
+    if (p == 0) o.s0 = (o.s0 & 0xFFFF0000u) | 0x0504u;
+    else if (p == 1) o.s0 = (o.s0 & 0x0000FFFFu) | 0x05040000u;
+    else if (p == 2) o.s1 = (o.s1 & 0xFFFF0000u) | 0x0504u;
+}
+
+static inline uint32_t pk_fld(uint32_t v, int pos) { return v << pos; }
+static inline uint32_t pk_sfld(int v, int pos, int bits) { return ((uint32_t)v & ((1u << bits) - 1u)) << pos; }
+
+// adder / flag helpers
+#define PK_F_Z 0x80u
+#define PK_F_N 0x40u
+#define PK_F_H 0x20u
+#define PK_F_C 0x10u
+
+static inline PkUop pk_uop_base(int len, int cyc) {
+    PkUop o;
+    o.d = pk_fld((uint32_t)len, PK_DB_LEN) | pk_fld((uint32_t)cyc / 4u, PK_DB_CYC) | pk_fld(8u, PK_DB_CPOS);
+    o.u = 0;
+    o.px = PK_PZERO;
+    o.py = PK_PZERO;
+    o.s0 = PK_S0_ID;
+    o.s1 = PK_S1_ID;
+    o.pa = PK_PZERO;
+    o.k = pk_fld(0xF0u, PK_KB_FKEEP);  // keep every flag unless the op says otherwise
+    return o;
+}
+static inline void pk_flags(PkUop& o, uint32_t keep, uint32_t cst) {
+    o.k = (o.k & ~(0xFFFFu << PK_KB_FKEEP)) | pk_fld(keep, PK_KB_FKEEP) | pk_fld(cst, PK_KB_FCONST);
+}
+static inline void pk_cond(PkUop& o, int cc) {  // NZ Z NC C
+    static const uint32_t pos[4] = {7, 7, 4, 4}, inv[4] = {1, 0, 1, 0};
+    o.d = (o.d & ~(15u << PK_DB_CPOS)) | pk_fld(pos[cc & 3], PK_DB_CPOS) | pk_fld(inv[cc & 3], PK_DB_CINV);
+}
+// memory operand through a register pair / (C) / SP / immediate
+static inline void pk_mem_pair(PkUop& o, int p) { o.pa = pk_sel16(p); }
+static inline void pk_mem_hc(PkUop& o) { o.pa = 0x0C0C0D00u; }  // 0xFF00 | C
+
+// 8-bit operation on A (or a register target) with source r / (HL) / n
+static inline void pk_alu(PkUop& o, int aop, int src) {
+    // src: 0..7 register (6 = (HL)), 8 = immediate n
+    o.px = pk_sel8(7);
+    if (src == 8) o.u |= pk_fld(1, PK_UB_YIMM) | pk_fld(1, PK_UB_IMM8);
+    else if (src == 6) o.u |= pk_fld(1, PK_UB_YMEM);
+    else o.py = pk_sel8(src);
+    o.u |= pk_fld(1, PK_UB_FZ);
+    if (aop <= 3 || aop == 7) {  // ADD ADC SUB SBC CP
+        o.u |= pk_fld(1, PK_UB_R8) | pk_fld(1, PK_UB_FH) | pk_fld(1, PK_UB_FC);
+        if (aop >= 2) o.u |= pk_fld(1, PK_UB_SUB);
+        if (aop == 1 || aop == 3) o.u |= pk_fld(1, PK_UB_USEC);
+        pk_flags(o, 0, aop >= 2 ? PK_F_N : 0);
+        if (aop != 7) pk_wb_r8(o, 7);
+    } else {  // AND XOR OR
+        o.u |= pk_fld(2, PK_UB_R8) | pk_fld((uint32_t)(aop - 4), PK_UB_LOP);
+        pk_flags(o, 0, aop == 4 ? PK_F_H : 0);
+        pk_wb_r8(o, 7);
+    }
+}
+
+static inline PkUop pk_uop(int op) {
+    PkUop o = pk_uop_base(1, 4);
+    const int N = 0;
+    (void)N;
+    if (op >= 0x40 && op < 0x80 && op != 0x76) {  // LD r, r'
+        int d = (op >> 3) & 7, s = op & 7;
+        o = pk_uop_base(1, (d == 6 || s == 6) ? 8 : 4);
+        if (s == 6) { o.u |= pk_fld(1, PK_UB_YMEM); o.d |= pk_fld(1, PK_DB_RD); pk_mem_pair(o, 2); }
+        else o.py = pk_sel8(s);
+        if (d == 6) { o.d |= pk_fld(1, PK_DB_WR); pk_mem_pair(o, 2); }
+        else pk_wb_r8(o, d);
+        return o;
+    }
+    if (op >= 0x80 && op < 0xC0) {  // ALU A, r
+        int s = op & 7;
+        o = pk_uop_base(1, s == 6 ? 8 : 4);
+        if (s == 6) { o.d |= pk_fld(1, PK_DB_RD); pk_mem_pair(o, 2); }
+        pk_alu(o, (op >> 3) & 7, s);
+        return o;
+    }
+    switch (op) {
+        case 0x00: return pk_uop_base(1, 4);
+        case 0x10: return pk_uop_base(2, 4);  // STOP: 2-byte no-op on DMG
+        case 0x76: o = pk_uop_base(0, 4); o.d |= pk_fld(1, PK_DB_HALT); return o;  // HALT: PC stays
+        case 0xF3: o.d |= pk_fld(1, PK_DB_IME); return o;
+        case 0xFB: o.d |= pk_fld(2, PK_DB_IME); return o;
+        case 0x27: o.d |= pk_fld(1, PK_DB_DAA); o.px = pk_sel8(7); pk_wb_r8(o, 7); return o;  // DAA (rare path)
+        case 0x2F:  // CPL = A ^ 0xFF
+            o.px = pk_sel8(7); o.k |= pk_fld(0xFF, PK_KB_YCONST);
+            o.u |= pk_fld(2, PK_UB_R8) | pk_fld(1, PK_UB_LOP);
+            pk_flags(o, PK_F_Z | PK_F_C, PK_F_N | PK_F_H); pk_wb_r8(o, 7); return o;
+        case 0x37: pk_flags(o, PK_F_Z, PK_F_C); return o;                                  // SCF
+        case 0x3F: pk_flags(o, PK_F_Z, 0); o.u |= pk_fld(3, PK_UB_FC); return o;          // CCF
+        case 0x07: case 0x0F: case 0x17: case 0x1F: {  // RLCA RRCA RLA RRA
+            int y = (op >> 3) & 3;
+            o.px = pk_sel8(7);
+            o.u |= pk_fld(3, PK_UB_R8) | pk_fld(2, PK_UB_FC) | pk_fld((uint32_t)(y & 1), PK_UB_RDIR)
+                 | pk_fld(y >= 2 ? 1u : 2u, PK_UB_RBIN);
+            pk_flags(o, 0, 0); pk_wb_r8(o, 7); return o;
+        }
+        case 0x08:  // LD (nn), SP
+            o = pk_uop_base(3, 20);
+            o.d |= pk_fld(1, PK_DB_WR) | pk_fld(1, PK_DB_WR2) | pk_fld(1, PK_DB_AIMM) | pk_sfld(1, PK_DB_ADIR, 2);
+            o.u |= pk_fld(1, PK_UB_W16) | pk_fld(1, PK_UB_WSP);
+            return o;
+        case 0x18: o = pk_uop_base(2, 12); o.d |= pk_fld(PK_T_JR, PK_DB_TSRC); return o;
+        case 0xC3: o = pk_uop_base(3, 16); o.d |= pk_fld(PK_T_IMM, PK_DB_TSRC); return o;
+        case 0xE9: o = pk_uop_base(1, 4); o.d |= pk_fld(PK_T_HL, PK_DB_TSRC); return o;
+        case 0xCD: case 0xC4: case 0xCC: case 0xD4: case 0xDC: {  // CALL (cc,) nn
+            o = pk_uop_base(3, op == 0xCD ? 24 : 12);
+            o.d |= pk_fld(PK_T_IMM, PK_DB_TSRC) | pk_fld(1, PK_DB_WR) | pk_fld(1, PK_DB_WR2) | pk_fld(1, PK_DB_ASP)
+                 | pk_sfld(-1, PK_DB_AOFF, 2) | pk_sfld(-1, PK_DB_ADIR, 2);
+            o.u |= pk_fld(1, PK_UB_W16) | pk_fld(1, PK_UB_WPC) | pk_sfld(-2, PK_UB_SPD, 3);
+            if (op != 0xCD) { pk_cond(o, (op >> 3) & 3); o.d |= pk_fld(3, PK_DB_XCYC); }
+            return o;
+        }
+        case 0xC9: case 0xD9: case 0xC0: case 0xC8: case 0xD0: case 0xD8: {  // RET / RETI / RET cc
+            o = pk_uop_base(1, (op == 0xC9 || op == 0xD9) ? 16 : 8);
+            o.d |= pk_fld(PK_T_M16, PK_DB_TSRC) | pk_fld(1, PK_DB_RD) | pk_fld(1, PK_DB_RD2) | pk_fld(1, PK_DB_ASP)
+                 | pk_sfld(1, PK_DB_ADIR, 2);
+            o.u |= pk_sfld(2, PK_UB_SPD, 3);
+            if (op == 0xD9) o.d |= pk_fld(2, PK_DB_IME);
+            if ((op & 0x0F) == 0x00 || (op & 0x0F) == 0x08) { pk_cond(o, (op >> 3) & 3); o.d |= pk_fld(3, PK_DB_XCYC); }
+            return o;
+        }
+        case 0xE0: case 0xF0: case 0xEA: case 0xFA: {  // LDH (n),A / LDH A,(n) / LD (nn),A / LD A,(nn)
+            int hn = (op & 0x0F) == 0x00;
+            o = pk_uop_base(hn ? 2 : 3, hn ? 12 : 16);
+            o.d |= pk_fld(1, PK_DB_AIMM) | pk_fld((uint32_t)hn, PK_DB_AHN);
+            if (op >= 0xF0) { o.d |= pk_fld(1, PK_DB_RD); o.u |= pk_fld(1, PK_UB_YMEM); pk_wb_r8(o, 7); }
+            else { o.d |= pk_fld(1, PK_DB_WR); o.py = pk_sel8(7); }
+            return o;
+        }
+        case 0xE2: case 0xF2:  // LD (C),A / LD A,(C)
+            o = pk_uop_base(1, 8);
+            pk_mem_hc(o);
+            if (op == 0xF2) { o.d |= pk_fld(1, PK_DB_RD); o.u |= pk_fld(1, PK_UB_YMEM); pk_wb_r8(o, 7); }
+            else { o.d |= pk_fld(1, PK_DB_WR); o.py = pk_sel8(7); }
+            return o;
+        case 0xE8: case 0xF8:  // ADD SP,e / LD HL,SP+e : X = SP, Y = sext(e), H/C from the low byte
+            o = pk_uop_base(2, op == 0xE8 ? 16 : 12);
+            o.u |= pk_fld(1, PK_UB_XSP) | pk_fld(1, PK_UB_YIMM) | pk_fld(1, PK_UB_SEXT) | pk_fld(1, PK_UB_FH) | pk_fld(1, PK_UB_FC);
+            pk_flags(o, 0, 0);
+            if (op == 0xE8) o.u |= pk_fld(1, PK_UB_SPW);
+            else pk_wb_r16(o, 2);
+            return o;
+        case 0xF9: o = pk_uop_base(1, 8); o.px = pk_sel16(2); o.u |= pk_fld(1, PK_UB_SPW); return o;  // LD SP,HL
+    }
+    // LD rr,nn / INC rr / DEC rr / ADD HL,rr / (BC|DE|HL+|HL-) loads and stores
+    if ((op & 0xC0) == 0x00) {
+        int p = (op >> 4) & 3, lo = op & 0x0F;
+        switch (lo) {
+            case 0x01:  // LD rr, nn
+                o = pk_uop_base(3, 12);
+                o.u |= pk_fld(1, PK_UB_YIMM);
+                if (p == 3) o.u |= pk_fld(1, PK_UB_SPW); else pk_wb_r16(o, p);
+                return o;
+            case 0x03: case 0x0B:  // INC rr / DEC rr
+                o = pk_uop_base(1, 8);
+                if (p == 3) o.u |= pk_fld(1, PK_UB_XSP) | pk_fld(1, PK_UB_SPW);
+                else { o.px = pk_sel16(p); pk_wb_r16(o, p); }
+                o.k |= pk_fld(1, PK_KB_YCONST);
+                if (lo == 0x0B) o.u |= pk_fld(1, PK_UB_SUB);
+                return o;
+            case 0x09:  // ADD HL, rr
+                o = pk_uop_base(1, 8);
+                o.px = pk_sel16(2);
+                if (p == 3) o.d |= pk_fld(1, PK_DB_YSP); else o.py = pk_sel16(p);
+                o.u |= pk_fld(1, PK_UB_HC16) | pk_fld(1, PK_UB_FH) | pk_fld(1, PK_UB_FC);
+                pk_flags(o, PK_F_Z, 0);
+                pk_wb_r16(o, 2);
+                return o;
+            case 0x02: case 0x0A: {  // LD (BC|DE|HL+|HL-), A  /  LD A, (...)
+                o = pk_uop_base(1, 8);
+                if (p < 2) pk_mem_pair(o, p);
+                else {
+                    pk_mem_pair(o, 2);
+                    o.u |= pk_sfld(p == 2 ? 1 : -1, PK_UB_HLINC, 2) | pk_fld(1, PK_UB_R16HL);
+                    pk_wb_r16(o, 2);
+                }
+                if (lo == 0x0A) { o.d |= pk_fld(1, PK_DB_RD); o.u |= pk_fld(1, PK_UB_YMEM); pk_wb_r8(o, 7); }
+                else { o.d |= pk_fld(1, PK_DB_WR); o.py = pk_sel8(7); }
+                return o;
+            }
+        }
+        int r = (op >> 3) & 7, low3 = op & 7;
+        if (low3 == 4 || low3 == 5) {  // INC r / DEC r
+            o = pk_uop_base(1, r == 6 ? 12 : 4);
+            if (r == 6) { o.d |= pk_fld(1, PK_DB_RD) | pk_fld(1, PK_DB_WR); pk_mem_pair(o, 2); o.u |= pk_fld(1, PK_UB_XMEM); }
+            else { o.px = pk_sel8(r); pk_wb_r8(o, r); }
+            o.k |= pk_fld(1, PK_KB_YCONST);
+            o.u |= pk_fld(1, PK_UB_R8) | pk_fld(1, PK_UB_FZ) | pk_fld(1, PK_UB_FH);
+            if (low3 == 5) o.u |= pk_fld(1, PK_UB_SUB);
+            pk_flags(o, PK_F_C, low3 == 5 ? PK_F_N : 0);
+            return o;
+        }
+        if (low3 == 6) {  // LD r, n
+            o = pk_uop_base(2, r == 6 ? 12 : 8);
+            o.u |= pk_fld(1, PK_UB_YIMM) | pk_fld(1, PK_UB_IMM8);
+            if (r == 6) { o.d |= pk_fld(1, PK_DB_WR); pk_mem_pair(o, 2); }
+            else pk_wb_r8(o, r);
+            return o;
+        }
+        if (low3 == 0 && op >= 0x20) {  // JR cc, e
+            o = pk_uop_base(2, 8);
+            o.d |= pk_fld(PK_T_JR, PK_DB_TSRC) | pk_fld(1, PK_DB_XCYC);
+            pk_cond(o, (op >> 3) & 3);
+            return o;
+        }
+    }
+    if ((op & 0xC0) == 0xC0) {
+        int p = (op >> 4) & 3, lo = op & 0x0F;
+        if (lo == 0x01) {  // POP rr
+            o = pk_uop_base(1, 12);
+            o.d |= pk_fld(1, PK_DB_RD) | pk_fld(1, PK_DB_RD2) | pk_fld(1, PK_DB_ASP) | pk_sfld(1, PK_DB_ADIR, 2);
+            o.u |= pk_fld(1, PK_UB_YMEM) | pk_sfld(2, PK_UB_SPD, 3);
+            if (p == 3) {  // POP AF: A <- m1, F <- m0 & 0xF0
+                o.u |= pk_fld(1, PK_UB_FPOP);
+                o.s1 = (o.s1 & 0x00FFFFFFu) | 0x05000000u;
+            } else pk_wb_r16(o, p);
+            return o;
+        }
+        if (lo == 0x05) {  // PUSH rr
+            o = pk_uop_base(1, 16);
+            o.d |= pk_fld(1, PK_DB_WR) | pk_fld(1, PK_DB_WR2) | pk_fld(1, PK_DB_ASP) | pk_sfld(-1, PK_DB_AOFF, 2)
+                 | pk_sfld(-1, PK_DB_ADIR, 2);
+            o.u |= pk_fld(1, PK_UB_W16) | pk_sfld(-2, PK_UB_SPD, 3);
+            o.py = pk_sel16(p);  // AF: F | A << 8
+            return o;
+        }
+        if ((op & 7) == 7) {  // RST
+            o = pk_uop_base(1, 16);
+            o.d |= pk_fld(PK_T_RST, PK_DB_TSRC) | pk_fld(1, PK_DB_WR) | pk_fld(1, PK_DB_WR2) | pk_fld(1, PK_DB_ASP)
+                 | pk_sfld(-1, PK_DB_AOFF, 2) | pk_sfld(-1, PK_DB_ADIR, 2);
+            o.u |= pk_fld(1, PK_UB_W16) | pk_fld(1, PK_UB_WPC) | pk_sfld(-2, PK_UB_SPD, 3);
+            return o;
+        }
+        if ((op & 7) == 6) {  // ALU A, n
+            o = pk_uop_base(2, 8);
+            pk_alu(o, (op >> 3) & 7, 8);
+            return o;
+        }
+        if ((op & 0xE7) == 0xC2) {  // JP cc, nn
+            o = pk_uop_base(3, 12);
+            o.d |= pk_fld(PK_T_IMM, PK_DB_TSRC) | pk_fld(1, PK_DB_XCYC);
+            pk_cond(o, (op >> 3) & 3);
+            return o;
+        }
+    }
+    // illegal opcode: freeze the CPU (documented extension; PyBoy raises)
+    o = pk_uop_base(0, 4);
+    o.d |= pk_fld(1, PK_DB_CRASH);
+    return o;
+}
+
+static inline PkUop pk_uop_cb(int op) {
+    int r = op & 7, y = (op >> 3) & 7, grp = op >> 6;
+    PkUop o = pk_uop_base(2, r == 6 ? (grp == 1 ? 12 : 16) : 8);
+    if (r == 6) {
+        pk_mem_pair(o, 2);
+        o.d |= pk_fld(1, PK_DB_RD);
+        if (grp != 1) o.d |= pk_fld(1, PK_DB_WR);
+        o.u |= pk_fld(1, PK_UB_XMEM);
+    } else {
+        o.px = pk_sel8(r);
+        if (grp != 1) pk_wb_r8(o, r);
+    }
+    switch (grp) {
+        case 0: {  // RLC RRC RL RR SLA SRA SWAP SRL
+            static const uint8_t dir[8] = {0, 1, 0, 1, 0, 1, 0, 1}, bin[8] = {2, 2, 1, 1, 0, 3, 0, 0};
+            o.u |= pk_fld(3, PK_UB_R8) | pk_fld(1, PK_UB_FZ) | pk_fld(dir[y], PK_UB_RDIR) | pk_fld(bin[y], PK_UB_RBIN);
+            if (y == 6) o.u |= pk_fld(1, PK_UB_SWAP);
+            else o.u |= pk_fld(2, PK_UB_FC);
+            pk_flags(o, 0, 0);
+            break;
+        }
+        case 1:  // BIT: Z = !(X & bit), H = 1, C kept
+            o.k |= pk_fld(1u << y, PK_KB_YCONST);
+            o.u |= pk_fld(2, PK_UB_R8) | pk_fld(0, PK_UB_LOP) | pk_fld(1, PK_UB_FZ);
+            pk_flags(o, PK_F_C, PK_F_H);
+            break;
+        case 2:  // RES = X & ~bit
+            o.k |= pk_fld(0xFFu & ~(1u << y), PK_KB_YCONST);
+            o.u |= pk_fld(2, PK_UB_R8) | pk_fld(0, PK_UB_LOP);
+            break;
+        default:  // SET = X | bit
+            o.k |= pk_fld(1u << y, PK_KB_YCONST);
+            o.u |= pk_fld(2, PK_UB_R8) | pk_fld(2, PK_UB_LOP);
+            break;
+    }
+    return o;
+}
+
+// the whole table: [0,256) base, [256,512) CB-prefixed, then the three pseudo-ops
+static inline void pk_build_ucode(uint32_t* t /* PK_UC_ENTRIES * 8 */) {
+    for (int i = 0; i < 512; i++) {
+        PkUop o = i < 256 ? pk_uop(i) : pk_uop_cb(i - 256);
+        if (i == 0xCB) o = pk_uop_base(2, 8);  // never executed: the kernel indexes 256 + second byte
+        uint32_t* e = t + (size_t)i * PK_UE_WORDS;
+        e[PK_UE_D] = o.d; e[PK_UE_U] = o.u; e[PK_UE_PX] = o.px; e[PK_UE_PY] = o.py;
+        e[PK_UE_S0] = o.s0; e[PK_UE_S1] = o.s1; e[PK_UE_PA] = o.pa; e[PK_UE_K] = o.k;
+    }
+    // INT: push PC (len 0: the current PC), jump to the vector the front-end puts in imm16, IME off
+    PkUop it = pk_uop_base(0, 0);
+    it.d |= pk_fld(PK_T_IMM, PK_DB_TSRC) | pk_fld(1, PK_DB_WR) | pk_fld(1, PK_DB_WR2) | pk_fld(1, PK_DB_ASP)
+          | pk_sfld(-1, PK_DB_AOFF, 2) | pk_sfld(-1, PK_DB_ADIR, 2) | pk_fld(1, PK_DB_IME);
+    it.u |= pk_fld(1, PK_UB_W16) | pk_fld(1, PK_UB_WPC) | pk_sfld(-2, PK_UB_SPD, 3);
+    PkUop idle = pk_uop_base(0, 4), nop0 = pk_uop_base(0, 0);
+    const PkUop ps[3] = {it, idle, nop0};
+    for (int j = 0; j < 3; j++) {
+        uint32_t* e = t + (size_t)(512 + j) * PK_UE_WORDS;
+        const PkUop& o = ps[j];
+        e[PK_UE_D] = o.d; e[PK_UE_U] = o.u; e[PK_UE_PX] = o.px; e[PK_UE_PY] = o.py;
+        e[PK_UE_S0] = o.s0; e[PK_UE_S1] = o.s1; e[PK_UE_PA] = o.pa; e[PK_UE_K] = o.k;
+    }
+}

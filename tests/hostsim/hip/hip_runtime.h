@@ -25,6 +25,25 @@
 #define __noinline__ __attribute__((noinline))
 #define __launch_bounds__(...)
 #define __builtin_amdgcn_readfirstlane(x) (x)
+// v_perm_b32: byte i of the result = byte sel.byte[i] of {hi, lo} (0-3 lo, 4-7 hi), 0x0C -> 0x00,
+// >= 0x0D -> 0xFF (8-11: sign replication, unused by the kernels)
+static inline uint32_t __builtin_amdgcn_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+    uint64_t v = ((uint64_t)hi << 32) | lo;
+    uint32_t r = 0;
+    for (int i = 0; i < 4; i++) {
+        uint32_t s = (sel >> (8 * i)) & 0xFFu, b;
+        if (s < 8) b = (uint32_t)(v >> (8 * s)) & 0xFFu;
+        else if (s == 0x0C) b = 0;
+        else if (s > 0x0C) b = 0xFF;
+        else abort();
+        r |= b << (8 * i);
+    }
+    return r;
+}
+// v_alignbyte_b32: ({hi, lo} >> (8 * (sh & 3)))[31:0]
+static inline uint32_t __builtin_amdgcn_alignbyte(uint32_t hi, uint32_t lo, uint32_t sh) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (sh & 3)));
+}
 using std::max;
 using std::min;
 
@@ -74,3 +93,7 @@ void pk_sim_launch(const char* name, dim3 grid, dim3 block, const std::function<
 // instruction trace for debugging (env, pc, w0, w1, sp, opcode)
 extern "C" void pk_sim_trace(uint32_t env, uint32_t pc, uint32_t w0, uint32_t w1, uint32_t sp, uint32_t op);
 #define PK_TRACE(env, pc, w0, w1, sp, op) pk_sim_trace(env, pc, w0, w1, sp, op)
+
+// per-iteration event bits (iteration statistics for kernel design; see pk_kernels.hip PK_EV_*)
+extern "C" void pk_sim_iter(uint32_t env, uint32_t ev);
+#define PK_ITER(env, ev) pk_sim_iter(env, ev)

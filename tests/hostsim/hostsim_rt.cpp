@@ -77,3 +77,21 @@ extern "C" uint64_t pk_sim_trace_get(uint32_t* out, uint64_t cap) {
     memcpy(out, g_trace.data(), n * 6 * 4);
     return n;
 }
+
+// ---- per-iteration event recording (PK_ITER) ----
+static std::vector<std::vector<uint32_t>> g_iter;
+static bool g_iter_on = false;
+extern "C" void pk_sim_iter_enable(uint32_t n_envs, int on) {
+    g_iter.assign(on ? n_envs : 0, {});
+    g_iter_on = on != 0;
+}
+extern "C" void pk_sim_iter(uint32_t env, uint32_t ev) {
+    if (!g_iter_on || env >= g_iter.size()) return;
+    g_iter[env].push_back(ev);   // one env is stepped by one thread: no lock needed
+}
+extern "C" uint64_t pk_sim_iter_get(uint32_t env, uint32_t* out, uint64_t cap) {
+    if (env >= g_iter.size()) return 0;
+    uint64_t n = g_iter[env].size();
+    if (out) memcpy(out, g_iter[env].data(), (n < cap ? n : cap) * 4);
+    return n;
+}
