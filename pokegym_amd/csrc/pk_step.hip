@@ -5,15 +5,17 @@
 // a restatement of PyBoy 1.x): cpu_tick / cpu_check_interrupts, cpu_execute, bus_read/bus_write,
 // lcd_tick, timer_tick, the HALT fast-forward of gb_tick.
 //
-// SIMT design (one wave = 64 independent emulators that drift apart within a few frames):
-//   * every lane runs the SAME instruction sequence per emulated instruction: front-end
+// SIMT design (one wave = 64 independent emulators that drift apart within a few frames, so any
+// path a lane takes more than ~1 % of the time is executed by the wave almost every iteration):
+//   * every lane runs the SAME straight-line sequence per emulated instruction: front-end
 //     (interrupts/HALT) -> fetch (LDS-staged ROM) -> microcode entry (LDS, pk_ucode.h) -> address
 //     -> read -> fused datapath -> register writeback (two v_perm_b32) -> write -> timer/LCD.
-//     Selections are written with sel() on precomputed values so the compiler emits v_cndmask,
-//     not divergent branch trees (the previous select-chain datapath compiled into ~600 SALU of
-//     exec-mask bookkeeping per emulated instruction).
-//   * only paths that a lane takes rarely (<1 % of iterations: special IO, MBC, OAM DMA, SRAM,
-//     deferred-line flush, frame end, DAA, timer overflow) are real branches.
+//     Selections are sel() on precomputed values (v_cndmask, not branch trees), and the hot loop
+//     has only single-level `if`s without `else`: LLVM's structurizer turns else-if chains into
+//     exec-mask bookkeeping that spilled SGPRs into VGPR lanes (measured: ~450 VALU per iteration).
+//   * paths a lane takes rarely (code outside the staged ROM, IO registers, MBC, OAM DMA, SRAM,
+//     deferred-line flush) are __noinline__ functions working on a copy of the lane state, so
+//     their code and registers stay out of the loop.
 //   * ROM bank 0 + the hottest switchable banks and the microcode table live in LDS; the RAM
 //     images are lane-interleaved in HBM (pk_layout.h) so lanes at the same guest address coalesce.
 #include <hip/hip_runtime.h>
@@ -28,6 +30,7 @@
 #define CPU_HALT 2u
 #define CPU_QUEUED 4u
 #define CPU_CRASH 8u
+#define PK_NO_BANK 0xFFFFFFFFu
 
 // debug hooks: the host-simulation build (tests/hostsim) records an instruction trace and
 // per-iteration event bits; the gfx950 build compiles them away.
@@ -46,6 +49,11 @@ enum {
     PK_EV_JUMP = 1u << 20, PK_EV_CB = 1u << 21, PK_EV_FAM0 = 1u << 22 /* 22..27: unused here */,
     PK_EV_RD_WRAM = 1u << 28, PK_EV_WR_WRAM = 1u << 29, PK_EV_WR_VRAM = 1u << 30, PK_EV_WR_HI = 1u << 31
 };
+
+// LDS, staged by each workgroup at kernel entry
+__shared__ __attribute__((aligned(16))) u32 lds_uc[PK_UC_ENTRIES * PK_UE_WORDS];  // microcode
+__shared__ __attribute__((aligned(16))) u8 lds_rom[PK_LDS_SLOTS * 0x4000u + 16u]; // ROM banks (+ fetch overrun pad)
+__shared__ int8_t lds_slot[128];                                                  // bank -> slot
 
 // ---------------------------------------------------------------------------------------------
 // branch-free helpers: arguments are evaluated unconditionally, so ?: on them is a v_cndmask
@@ -66,17 +74,16 @@ struct St {
     u32 timac;            // TIMA_counter
     u32 mbc;              // rombank | rambank<<8 | ram_enabled<<16 | memorymodel<<24
     u32 misc;             // joypad directional | standard<<8 | (ly_window+1)<<16
-    u32 rb;               // LDS byte offset of the switchable ROM bank, 0xFFFFFFFF = not staged
+    u32 rb;               // LDS byte offset of the switchable ROM bank, PK_NO_BANK = not staged
     u32 npend;            // latched, not yet rasterised lines
     u32 render, blank, frame_done;
 };
 
+// where this lane's emulator lives
 struct Ctx {
     const PkStepArgs* A;
     u8* g;                // lane-interleaved RAM image of this wave's group
     u32 lane, env, gid;
-    const u8* lds_rom;
-    const int8_t* lds_slot;
 };
 
 __device__ __forceinline__ u32 ld_img(const Ctx& c, u32 phys) { return c.g[phys * PK_LANES + c.lane]; }
@@ -92,19 +99,13 @@ __device__ __forceinline__ u32 fast_phys(u32 a) {
     const u32 p = (a & 0x1FFFu) + sel(a < 0xA000u, PK_P_VRAM, PK_P_WRAM);
     return sel(a >= 0xFE00u, PK_P_OAM + (a & 0x1FFu), p);
 }
-
-__device__ __forceinline__ u32 rom_bank(const Ctx& c, const St& s, u32 a) {
-    return sel(a < 0x4000u, 0u, (s.mbc & 0xFFu) & c.A->rom_bank_mask);
-}
-__device__ __forceinline__ u32 rom_read(const Ctx& c, const St& s, u32 a) {
-    const u32 off = a & 0x3FFFu;
-    if (a < 0x4000u) return c.lds_rom[a];
-    if (s.rb != 0xFFFFFFFFu) return c.lds_rom[s.rb + off];
-    return c.A->rom[rom_bank(c, s, a) * 0x4000u + off];
-}
-__device__ __forceinline__ u32 slot_base(const Ctx& c, u32 bank) {
-    const int sl = c.lds_slot[bank & 127u];
-    return sl >= 0 ? (u32)sl * 0x4000u : 0xFFFFFFFFu;
+__device__ __forceinline__ bool vram_or_oam(u32 a) { return (a >= 0x8000u && a < 0xA000u) || (a >= 0xFE00u && a < 0xFEA0u); }
+// ROM address staged in LDS?  and its LDS byte index
+__device__ __forceinline__ bool rom_staged(const St& s, u32 a) { return a < 0x4000u || (a < 0x8000u && s.rb != PK_NO_BANK); }
+__device__ __forceinline__ u32 rom_lds_index(const St& s, u32 a) { return sel(a < 0x4000u, a, s.rb + (a & 0x3FFFu)); }
+__device__ __forceinline__ u32 slot_base(u32 bank) {
+    const int sl = lds_slot[bank & 127u];
+    return sl >= 0 ? (u32)sl * 0x4000u : PK_NO_BANK;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -130,6 +131,14 @@ __device__ __forceinline__ void key_event(St& s, u32 button, bool pressed) {
     if (((od ^ nd) & od) || ((os ^ ns) & os)) s.cpu |= 0x10u << 16;
 }
 
+// ---------------------------------------------------------------------------------------------
+// generic memory bus (rare paths only)
+__device__ __forceinline__ u32 rom_read(const Ctx& c, const St& s, u32 a) {
+    if (rom_staged(s, a)) return lds_rom[rom_lds_index(s, a)];
+    const u32 bank = (s.mbc & 0xFFu) & c.A->rom_bank_mask;
+    return c.A->rom[bank * 0x4000u + (a & 0x3FFFu)];
+}
+
 // IO register read (FF00-FF7F, FFFF) — oracle: gbcore.c bus_read
 __device__ __forceinline__ u32 io_read(const Ctx& c, const St& s, u32 a) {
     if (a == 0xFFFFu) return bfe8(s.cpu, 8);
@@ -153,7 +162,7 @@ __device__ __forceinline__ u32 io_read(const Ctx& c, const St& s, u32 a) {
     return v;
 }
 
-// generic bus read (pyboy mb.getitem) — any address, used off the fast paths
+// pyboy mb.getitem for any address
 __device__ __forceinline__ u32 bus_read_any(const Ctx& c, const St& s, u32 a) {
     if (a < 0x8000u) return rom_read(c, s, a);
     if ((a & 0xE000u) == 0xA000u) {  // cartridge SRAM
@@ -164,8 +173,8 @@ __device__ __forceinline__ u32 bus_read_any(const Ctx& c, const St& s, u32 a) {
     return ld_img(c, fast_phys(a));
 }
 
-// generic bus write (pyboy mb.setitem): MBC3 registers, SRAM, IO registers, OAM DMA, IE, and
-// plain RAM (with the deferred-line flush before VRAM/OAM changes)
+// pyboy mb.setitem for any address: MBC3 registers, SRAM, IO registers, OAM DMA, IE, and plain
+// RAM (with the deferred-line flush before VRAM/OAM changes)
 __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v) {
     const PkStepArgs& A = *c.A;
     if (a < 0x8000u) {  // MBC3.setitem
@@ -175,7 +184,7 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
         } else if (a < 0x4000u) {
             v &= 0x7Fu;
             s.mbc = setb8(s.mbc, 0, v == 0u ? 1u : v);
-            s.rb = slot_base(c, (s.mbc & 0xFFu) & A.rom_bank_mask);
+            s.rb = slot_base((s.mbc & 0xFFu) & A.rom_bank_mask);
         } else if (a < 0x6000u) {
             s.mbc = setb8(s.mbc, 8, v);
         }
@@ -227,19 +236,42 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
         }
         return;
     }
-    if (s.npend && (a < 0xA000u || (a >= 0xFE00u && a < 0xFEA0u))) {
+    if (s.npend && vram_or_oam(a)) {
         flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.env, c.gid);
         s.npend = 0;
     }
     st_img(c, fast_phys(a), v);
 }
 
+// ---- out-of-line rare paths (operate on a copy of the lane state) ----
+__device__ __forceinline__ u32 pk_fetch_slow(const PkStepArgs* A, u8* g, u32 lane, const St* sp, u32 pc) {
+    Ctx c;
+    c.A = A; c.g = g; c.lane = lane; c.env = 0; c.gid = 0;
+    const St s = *sp;
+    return bus_read_any(c, s, pc) | (bus_read_any(c, s, (pc + 1u) & 0xFFFFu) << 8)
+         | (bus_read_any(c, s, (pc + 2u) & 0xFFFFu) << 16);
+}
+__device__ __forceinline__ u32 pk_read_slow(const PkStepArgs* A, u8* g, u32 lane, const St* sp, u32 a0, u32 a1, u32 two) {
+    Ctx c;
+    c.A = A; c.g = g; c.lane = lane; c.env = 0; c.gid = 0;
+    const St s = *sp;
+    const u32 m0 = bus_read_any(c, s, a0);
+    const u32 m1 = two ? bus_read_any(c, s, a1) : 0u;
+    return m0 | (m1 << 8);
+}
+__device__ __forceinline__ void pk_write_slow(const PkStepArgs* A, u8* g, u32 lane, u32 env, u32 gid, St* sp,
+                                                  u32 a0, u32 v0, u32 a1, u32 v1, u32 two) {
+    Ctx c;
+    c.A = A; c.g = g; c.lane = lane; c.env = env; c.gid = gid;
+    St s = *sp;
+    bus_write_any(c, s, a0, v0);
+    if (two) bus_write_any(c, s, a1, v1);
+    *sp = s;
+}
+
 // ---------------------------------------------------------------------------------------------
 // K1
 __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
-    __shared__ __attribute__((aligned(16))) u32 lds_uc[PK_UC_ENTRIES * PK_UE_WORDS];
-    __shared__ __attribute__((aligned(16))) u8 lds_rom[PK_LDS_SLOTS * 0x4000u];
-    __shared__ int8_t lds_slot[128];
     for (u32 i = threadIdx.x; i < PK_UC_ENTRIES * PK_UE_WORDS; i += blockDim.x) lds_uc[i] = A.ucode[i];
     for (u32 i = threadIdx.x; i < 128u; i += blockDim.x) lds_slot[i] = A.bank_slot[i];
     for (u32 sl = 0; sl < A.nslots; sl++) {
@@ -262,8 +294,6 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
     c.env = env;
     c.gid = __builtin_amdgcn_readfirstlane(env / PK_LANES);
     c.g = A.mem + (size_t)c.gid * PK_GROUP_STRIDE;
-    c.lds_rom = lds_rom;
-    c.lds_slot = lds_slot;
 
     const u32 np = A.npad;
     u32* R = A.regs;
@@ -286,7 +316,7 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
     }
     s.mbc = R[PK_R_MBC * np + env];
     s.misc = R[PK_R_MISC * np + env];
-    s.rb = slot_base(c, (s.mbc & 0xFFu) & A.rom_bank_mask);
+    s.rb = slot_base((s.mbc & 0xFFu) & A.rom_bank_mask);
     s.npend = 0;
     s.blank = 0;
     s.frame_done = 0;
@@ -325,33 +355,25 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
         const u32 pc = (s.pc + sel((doint && halted) || wake, 1u, 0u)) & 0xFFFFu;
         const u32 intflag = pend & (0u - pend);
         s.cpu = sel(doint, (cpu0 | CPU_QUEUED) & ~CPU_HALT, sel(wake, cpu0 & ~CPU_HALT, cpu0)) ^ sel(dispatch, intflag << 16, 0u);
-        u32 di = sel(dispatch, PK_UC_INT, sel(doint, PK_UC_NOP0, PK_UC_IDLE));
-        u32 bytes = (0x40u + 8u * (u32)__builtin_ctz(intflag | 0x20u)) << 8;  // INT: vector as imm16
 
-        // ---------------- fetch: LDS-staged ROM, else the RAM image / generic bus ----------------
-        if (exec) {
-            const u32 off = pc & 0x3FFFu;
-            if (pc < 0x8000u && (pc < 0x4000u || s.rb != 0xFFFFFFFFu) && off < 0x3FFEu) {
-                const u32 la = sel(pc < 0x4000u, pc, s.rb + off);
-                bytes = __builtin_amdgcn_alignbyte(romw[(la >> 2) + 1u], romw[la >> 2], la & 3u);
-                ev |= PK_EV_F_LDS;
-            } else if (fast_ram(pc) && fast_ram((pc + 2u) & 0xFFFFu) && ((pc ^ (pc + 2u)) & 0xFE00u) == 0u) {
-                const u32 p = fast_phys(pc);  // code in RAM (e.g. the HRAM OAM-DMA wait loop)
-                bytes = ld_img(c, p) | (ld_img(c, p + 1u) << 8) | (ld_img(c, p + 2u) << 16);
-                ev |= PK_EV_F_BUS | sel(pc >= 0xFF80u, PK_EV_HRAM, 0u);
-            } else {
-                bytes = bus_read_any(c, s, pc) | (bus_read_any(c, s, (pc + 1u) & 0xFFFFu) << 8)
-                      | (bus_read_any(c, s, (pc + 2u) & 0xFFFFu) << 16);
-                ev |= sel(pc < 0x8000u, PK_EV_F_ROM16, PK_EV_F_BUS);
-            }
-            const u32 op = bytes & 0xFFu;
-            di = sel(op == 0xCBu, 256u + ((bytes >> 8) & 0xFFu), op);
-            icount += 1u;
-            ev |= PK_EV_EXEC | sel(op == 0xCBu, PK_EV_CB, 0u);
-            PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, op);
+        // ---------------- fetch: LDS-staged ROM for every lane; other code out of line ----------------
+        const bool flds = rom_staged(s, pc) && (pc & 0x3FFFu) < 0x3FFEu;
+        const u32 la = sel(flds, rom_lds_index(s, pc), 0u);
+        u32 bytes = __builtin_amdgcn_alignbyte(romw[(la >> 2) + 1u], romw[la >> 2], la & 3u);
+        if (exec && !flds) {
+            const St t = s;
+            bytes = pk_fetch_slow(&A, c.g, c.lane, &t, pc);
+            ev |= PK_EV_F_BUS | sel(pc >= 0xFF80u, PK_EV_HRAM, 0u);
         }
-        if (dispatch) ev |= PK_EV_INT;
-        if (!exec && !dispatch) ev |= PK_EV_IDLE;
+        const u32 op = bytes & 0xFFu;
+        // INT pseudo-op: the vector rides in imm16
+        bytes = sel(exec, bytes, (0x40u + 8u * (u32)__builtin_ctz(intflag | 0x20u)) << 8);
+        const u32 di = sel(exec, sel(op == 0xCBu, 256u + ((bytes >> 8) & 0xFFu), op),
+                           sel(dispatch, PK_UC_INT, sel(doint, PK_UC_NOP0, PK_UC_IDLE)));
+        icount += sel(exec, 1u, 0u);
+        ev |= sel(exec, PK_EV_EXEC | sel(flds, PK_EV_F_LDS, 0u) | sel(op == 0xCBu, PK_EV_CB, 0u), 0u)
+            | sel(dispatch, PK_EV_INT, 0u) | sel(!exec && !dispatch, PK_EV_IDLE, 0u);
+        if (exec) PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, op);
         const uint4 e0 = ucv[di * 2u], e1 = ucv[di * 2u + 1u];
         const u32 D = e0.x, U = e0.y, PX = e0.z, PY = e0.w, S0 = e1.x, S1 = e1.y, PA = e1.z, K = e1.w;
 
@@ -371,26 +393,28 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
         const u32 addr1 = (addr0 + (u32)sfield(D, PK_DB_ADIR, 2)) & 0xFFFFu;
 
         // ---------------- memory reads (m0 at addr0, m1 at addr1) ----------------
+        const bool rd = bit(D, PK_DB_RD) != 0u, rd2 = bit(D, PK_DB_RD2) != 0u;
+        const bool rram = rd && fast_ram(addr0) && fast_ram(addr1);  // addr1 == addr0 for 1-byte reads
+        const bool rrom = rd && rom_staged(s, addr0) && rom_staged(s, addr1);
         u32 m0 = 0, m1 = 0;
-        const bool rd2 = bit(D, PK_DB_RD2) != 0u;
-        if (bit(D, PK_DB_RD)) {
-            const bool f0 = fast_ram(addr0), f1 = !rd2 || fast_ram(addr1);
-            if (f0 && f1) {
-                m0 = ld_img(c, fast_phys(addr0));
-                if (rd2) m1 = ld_img(c, fast_phys(addr1));
-                ev |= PK_EV_RD_RAM;
-            } else if (addr0 < 0x8000u && (!rd2 || addr1 < 0x8000u)) {
-                m0 = rom_read(c, s, addr0);
-                if (rd2) m1 = rom_read(c, s, addr1);
-                ev |= PK_EV_RD_ROMLDS;
-            } else {
-                m0 = bus_read_any(c, s, addr0);
-                if (rd2) m1 = bus_read_any(c, s, addr1);
-                ev |= PK_EV_RD_IO;
-            }
-            ev |= PK_EV_RD | sel(rd2, PK_EV_RD2, 0u) | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
-                | sel(addr0 >= 0xC000u && addr0 < 0xFE00u, PK_EV_RD_WRAM, 0u);
+        if (rram) {
+            m0 = ld_img(c, fast_phys(addr0));
+            if (rd2) m1 = ld_img(c, fast_phys(addr1));
         }
+        if (rrom) {
+            m0 = lds_rom[rom_lds_index(s, addr0)];
+            m1 = sel(rd2, (u32)lds_rom[rom_lds_index(s, addr1)], 0u);
+        }
+        if (rd && !rram && !rrom) {
+            const St t = s;
+            const u32 m = pk_read_slow(&A, c.g, c.lane, &t, addr0, addr1, rd2 ? 1u : 0u);
+            m0 = m & 0xFFu;
+            m1 = m >> 8;
+            ev |= PK_EV_RD_IO;
+        }
+        ev |= sel(rd, PK_EV_RD | sel(rd2, PK_EV_RD2, 0u) | sel(rram, PK_EV_RD_RAM, 0u) | sel(rrom, PK_EV_RD_ROMLDS, 0u)
+                      | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
+                      | sel(addr0 >= 0xC000u && addr0 < 0xFE00u, PK_EV_RD_WRAM, 0u), 0u);
         const u32 m16 = m0 | (m1 << 8);
 
         // ---------------- fused datapath ----------------
@@ -431,10 +455,10 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
         nf = sel(bit(U, PK_UB_FPOP), m0 & 0xF0u, nf) & 0xFFu;
         if (bit(D, PK_DB_DAA)) {  // DAA (opcodes.py DAA_27), rare
             const u32 a = w1 >> 24;
-            u32 corr = ((F & 0x20u) ? 0x06u : 0u) | ((F & 0x10u) ? 0x60u : 0u);
-            if (!(F & 0x40u)) corr |= ((a & 0x0Fu) > 0x09u ? 0x06u : 0u) | (a > 0x99u ? 0x60u : 0u);
-            res8 = ((F & 0x40u) ? (a - corr) : (a + corr)) & 0xFFu;
-            nf = (F & 0x40u) | (res8 == 0u ? 0x80u : 0u) | ((corr & 0x60u) ? 0x10u : 0u);
+            u32 corr = sel(F & 0x20u, 0x06u, 0u) | sel(F & 0x10u, 0x60u, 0u);
+            corr |= sel(F & 0x40u, 0u, sel((a & 0x0Fu) > 0x09u, 0x06u, 0u) | sel(a > 0x99u, 0x60u, 0u));
+            res8 = sel(F & 0x40u, a - corr, a + corr) & 0xFFu;
+            nf = (F & 0x40u) | sel(res8 == 0u, 0x80u, 0u) | sel(corr & 0x60u, 0x10u, 0u);
         }
         // register writeback: val = res16 | F' << 16 | res8 << 24 through the per-op byte selectors
         const u32 val = res16 | (nf << 16) | (res8 << 24);
@@ -447,7 +471,7 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
         const u32 tgt = sel(tsrc == PK_T_IMM, imm16, sel(tsrc == PK_T_HL, hl, sel(tsrc == PK_T_JR, jrt, sel(tsrc == PK_T_M16, m16, bytes & 0x38u))));
         const bool jump = tsrc != 0u && taken != 0u;
         s.pc = sel(jump, tgt, pcn);
-        if (jump) ev |= PK_EV_JUMP;
+        ev |= sel(jump, PK_EV_JUMP, 0u);
         u32 cycles = ((D >> PK_DB_CYC) & 7u) * 4u + sel(taken != 0u, ((D >> PK_DB_XCYC) & 3u) * 4u, 0u);
         const u32 sp2 = (sp + ((u32)sfield(U, PK_UB_SPD, 3) & (0u - taken))) & 0xFFFFu;
         s.sp = sel(bit(U, PK_UB_SPW), res16, sp2);
@@ -460,114 +484,103 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
         }
 
         // ---------------- memory writes (wv0 at addr0, wv1 at addr1) ----------------
-        if (bit(D, PK_DB_WR) && taken) {
-            const bool wr2 = bit(D, PK_DB_WR2) != 0u;
-            const u32 pushv = sel(bit(U, PK_UB_WPC), pcn, sel(bit(U, PK_UB_WSP), sp, Y & 0xFFFFu));
-            const u32 wv = sel(bit(U, PK_UB_W16), pushv, res8);
-            const bool hifirst = bit(D, PK_DB_ADIR + 1) != 0u;  // adir = -1: push writes the high byte first
-            const u32 wv0 = sel(hifirst, wv >> 8, wv) & 0xFFu, wv1 = sel(hifirst, wv, wv >> 8) & 0xFFu;
-            const bool f0 = fast_ram(addr0), f1 = !wr2 || fast_ram(addr1);
-            ev |= PK_EV_WR | sel(wr2, PK_EV_WR2, 0u) | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
-                | sel(addr0 >= 0xC000u && addr0 < 0xFE00u, PK_EV_WR_WRAM, sel(addr0 >= 0x8000u && addr0 < 0xA000u, PK_EV_WR_VRAM, 0u));
-            if (f0 && f1) {
-                if (s.npend) {
-                    const bool vo0 = addr0 < 0xA000u || (addr0 >= 0xFE00u && addr0 < 0xFEA0u);
-                    const bool vo1 = wr2 && (addr1 < 0xA000u || (addr1 >= 0xFE00u && addr1 < 0xFEA0u));
-                    if (vo0 || vo1) {
-                        flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, env, c.gid);
-                        s.npend = 0;
-                        ev |= PK_EV_FLUSH;
-                    }
-                }
-                st_img(c, fast_phys(addr0), wv0);
-                if (wr2) st_img(c, fast_phys(addr1), wv1);
-            } else {
-                bus_write_any(c, s, addr0, wv0);
-                if (wr2) bus_write_any(c, s, addr1, wv1);
-                ev |= PK_EV_WR_SLOW;
-            }
+        const bool wr = bit(D, PK_DB_WR) != 0u && taken != 0u, wr2 = bit(D, PK_DB_WR2) != 0u;
+        const u32 pushv = sel(bit(U, PK_UB_WPC), pcn, sel(bit(U, PK_UB_WSP), sp, Y & 0xFFFFu));
+        const u32 wv = sel(bit(U, PK_UB_W16), pushv, res8);
+        const bool hifirst = bit(D, PK_DB_ADIR + 1) != 0u;  // adir = -1: push writes the high byte first
+        const u32 wv0 = sel(hifirst, wv >> 8, wv) & 0xFFu, wv1 = sel(hifirst, wv, wv >> 8) & 0xFFu;
+        const bool wvo = s.npend != 0u && (vram_or_oam(addr0) || (wr2 && vram_or_oam(addr1)));
+        const bool wram = wr && fast_ram(addr0) && fast_ram(addr1) && !wvo;
+        if (wram) {
+            st_img(c, fast_phys(addr0), wv0);
+            if (wr2) st_img(c, fast_phys(addr1), wv1);
         }
+        if (wr && !wram) {  // IO / MBC / SRAM / OAM DMA / flush before VRAM-OAM: out of line
+            St t = s;
+            pk_write_slow(&A, c.g, c.lane, env, c.gid, &t, addr0, wv0, addr1, wv1, wr2 ? 1u : 0u);
+            s = t;
+            ev |= PK_EV_WR_SLOW | sel(wvo, PK_EV_FLUSH, 0u);
+        }
+        ev |= sel(wr, PK_EV_WR | sel(wr2, PK_EV_WR2, 0u) | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
+                      | sel(addr0 >= 0xC000u && addr0 < 0xFE00u, PK_EV_WR_WRAM, sel(addr0 >= 0x8000u && addr0 < 0xA000u, PK_EV_WR_VRAM, 0u)), 0u);
 
         // ---------------- HALT fast-forward, timer, LCD (pyboy mb.tick) ----------------
+        const u32 tac = s.tim0 >> 24;
+        const u32 dsh = sel((tac & 3u) == 0u, 10u, sel((tac & 3u) == 1u, 4u, sel((tac & 3u) == 2u, 6u, 8u)));
         if (s.cpu & CPU_HALT) {
-            const u32 tac = s.tim0 >> 24;
-            const u32 dsh = sel((tac & 3u) == 0u, 10u, sel((tac & 3u) == 1u, 4u, sel((tac & 3u) == 2u, 6u, 8u)));
-            const int tb = (tac & 4u) ? (int)((0x100u - bfe8(s.tim0, 8)) << dsh) - (int)s.timac : (1 << 16);
+            const int tb = (int)sel(tac & 4u, ((0x100u - bfe8(s.tim0, 8)) << dsh) - s.timac, 1u << 16);
             const int ta = (int)s.target - (int)s.clock;
             const int mm = ta < tb ? ta : tb;
-            cycles = mm < 0 ? 0u : (u32)mm;
+            cycles = (u32)(mm < 0 ? 0 : mm);
         }
         u32 irq = 0;
         s.divacc = (s.divacc + cycles) & 0xFFFFu;
-        if (s.tim0 & 0x04000000u) {  // TAC enabled (timer.py Timer.tick)
-            const u32 tac = s.tim0 >> 24;
-            const u32 dsh = sel((tac & 3u) == 0u, 10u, sel((tac & 3u) == 1u, 4u, sel((tac & 3u) == 2u, 6u, 8u)));
+        if (tac & 4u) {  // TAC enabled (timer.py Timer.tick)
             u32 timac = s.timac + cycles;
             u32 tima = bfe8(s.tim0, 8);
-            if (timac >= (1u << dsh)) {
-                const u32 mul = timac >> dsh;
-                timac -= mul << dsh;
-                tima += mul;
-                if (tima > 0xFFu) {
-                    tima = (tima - 0x100u + bfe8(s.tim0, 16)) & 0xFFu;
-                    irq |= 4u;
-                    ev |= PK_EV_TIMER;
-                }
-            }
+            const u32 mul = timac >> dsh;
+            timac -= mul << dsh;
+            tima += mul;
+            const bool ovf = tima > 0xFFu;
+            tima = sel(ovf, (tima - 0x100u + bfe8(s.tim0, 16)) & 0xFFu, tima);
+            irq |= sel(ovf, 4u, 0u);
+            ev |= sel(ovf, PK_EV_TIMER, 0u);
             s.tim0 = setb8(s.tim0, 8, tima);
             s.timac = timac;
         }
         s.clock += cycles;
         const u32 lcdc = s.lcd0 & 0xFFu;
-        if (lcdc & 0x80u) {
-            if (s.clock >= s.target) {  // lcd.tick mode transition
-                ev |= PK_EV_LCD;
-                const u32 nm = s.lcd2 >> 24;
-                u32 stat = bfe8(s.lcd0, 8), ly = bfe8(s.lcd0, 16);
-                const u32 lyc = s.lcd0 >> 24;
-                const bool changed = (stat & 3u) != nm;
-                stat = (stat & 0xFCu) | nm;
-                irq |= sel(changed && nm != 3u && ((stat >> (nm + 3u)) & 1u), 2u, 0u);
-                const bool m2 = nm == 2u, m3 = nm == 3u, m0 = nm == 0u, m1 = nm == 1u;
-                const bool wrap = m2 && ly == 153u;
-                if (wrap) {
-                    s.clock %= FRAME_CYCLES;
-                    s.target %= FRAME_CYCLES;
-                }
-                ly = sel(wrap, 0u, sel(m2 || m1, ly + 1u, ly));
-                s.target += sel(m2, 80u, sel(m3, 170u, sel(m0, 206u, 456u)));
-                const bool eq = lyc == ly, upd = m2 || m1;
-                stat = sel(upd, sel(eq, stat | 4u, stat & 0xFBu), stat);
-                irq |= sel(upd && eq && (stat & 0x40u), 2u, 0u);
-                const u32 nnext = sel(m2, 3u, sel(m3, 0u, sel(m0, sel(ly < 143u, 2u, 1u), sel(ly == 153u, 2u, 1u))));
-                const bool vbl = m1 && ly == 144u;
-                irq |= sel(vbl, 1u, 0u);
-                s.frame_done |= sel(vbl, 1u, 0u);
-                s.lcd0 = (s.lcd0 & 0xFF0000FFu) | (stat << 8) | (ly << 16);
-                s.lcd2 = (s.lcd2 & 0x00FFFFFFu) | (nnext << 24);
-                if (m0 && s.render && ly < PK_ROWS) {
-                    // latch this scanline's registers; rasterised by K2 (or flush_lines)
-                    const u32 wy = bfe8(s.lcd1, 16), wx = bfe8(s.lcd1, 24);
-                    int lw = (int)bfe8(s.misc, 16) - 1;
-                    if ((lcdc & 0x20u) && wy <= ly && (int)wx - 7 < (int)PK_COLS) lw += 1;
-                    const u32 idx = (c.gid * PK_ROWS + ly) * PK_LANES + c.lane;
-                    A.lat[idx] = lcdc | (bfe8(s.lcd1, 8) << 8) | (bfe8(s.lcd1, 0) << 16) | (wx << 24);
-                    A.lat[A.lat_stride + idx] = wy | ((s.lcd2 & 0xFFFFFFu) << 8);
-                    A.lat[2u * A.lat_stride + idx] = (u32)(lw + 1) | 0x100u;
-                    if (ly == PK_ROWS - 1u) lw = -1;
-                    s.misc = setb8(s.misc, 16, (u32)(lw + 1));
-                    s.npend += 1u;
-                }
+        const bool lcdev = (lcdc & 0x80u) && s.clock >= s.target;
+        if (lcdev) {  // lcd.tick mode transition
+            const u32 nm = s.lcd2 >> 24;
+            u32 stat = bfe8(s.lcd0, 8), ly = bfe8(s.lcd0, 16);
+            const u32 lyc = s.lcd0 >> 24;
+            const bool changed = (stat & 3u) != nm;
+            stat = (stat & 0xFCu) | nm;
+            irq |= sel(changed && nm != 3u && ((stat >> (nm + 3u)) & 1u), 2u, 0u);
+            const bool m2 = nm == 2u, m3 = nm == 3u, m0 = nm == 0u, m1 = nm == 1u;
+            const bool wrap = m2 && ly == 153u;  // clock, target < 2 frames: one subtraction
+            s.clock -= sel(wrap && s.clock >= FRAME_CYCLES, FRAME_CYCLES, 0u);
+            s.target -= sel(wrap && s.target >= FRAME_CYCLES, FRAME_CYCLES, 0u);
+            ly = sel(wrap, 0u, sel(m2 || m1, ly + 1u, ly));
+            s.target += sel(m2, 80u, sel(m3, 170u, sel(m0, 206u, 456u)));
+            const bool eq = lyc == ly, upd = m2 || m1;
+            stat = sel(upd, sel(eq, stat | 4u, stat & 0xFBu), stat);
+            irq |= sel(upd && eq && (stat & 0x40u), 2u, 0u);
+            const u32 nnext = sel(m2, 3u, sel(m3, 0u, sel(m0, sel(ly < 143u, 2u, 1u), sel(ly == 153u, 2u, 1u))));
+            const bool vbl = m1 && ly == 144u;
+            irq |= sel(vbl, 1u, 0u);
+            s.frame_done |= sel(vbl, 1u, 0u);
+            s.lcd0 = (s.lcd0 & 0xFF0000FFu) | (stat << 8) | (ly << 16);
+            s.lcd2 = (s.lcd2 & 0x00FFFFFFu) | (nnext << 24);
+        }
+        ev |= sel(lcdev, PK_EV_LCD, 0u);
+        {
+            // latch this scanline's registers at its mode-0 event in the rendered frame; K2 (or
+            // flush_lines) rasterises it later
+            const u32 ly = bfe8(s.lcd0, 16);
+            if (lcdev && s.render && (s.lcd0 & 0x300u) == 0u && ly < PK_ROWS) {
+                const u32 wy = bfe8(s.lcd1, 16), wx = bfe8(s.lcd1, 24);
+                int lw = (int)bfe8(s.misc, 16) - 1;
+                if ((lcdc & 0x20u) && wy <= ly && (int)wx - 7 < (int)PK_COLS) lw += 1;
+                const u32 idx = (c.gid * PK_ROWS + ly) * PK_LANES + c.lane;
+                A.lat[idx] = lcdc | (bfe8(s.lcd1, 8) << 8) | (bfe8(s.lcd1, 0) << 16) | (wx << 24);
+                A.lat[A.lat_stride + idx] = wy | ((s.lcd2 & 0xFFFFFFu) << 8);
+                A.lat[2u * A.lat_stride + idx] = (u32)(lw + 1) | 0x100u;
+                if (ly == PK_ROWS - 1u) lw = -1;
+                s.misc = setb8(s.misc, 16, (u32)(lw + 1));
+                s.npend += 1u;
             }
-        } else if (s.clock >= FRAME_CYCLES) {
+        }
+        if (!(lcdc & 0x80u) && s.clock >= FRAME_CYCLES) {  // LCD off: the frame ends on the clock alone
             s.frame_done = 1u;
             s.clock %= FRAME_CYCLES;
-            if (s.render) s.blank = 1u;
+            s.blank |= s.render;
         }
         s.cpu |= irq << 16;
         budget += cycles + 1u;
-        if (budget > 16u * FRAME_CYCLES) s.frame_done = 1u;
-        if (s.frame_done) ev |= PK_EV_FRAME;
+        s.frame_done |= sel(budget > 16u * FRAME_CYCLES, 1u, 0u);
+        ev |= sel(s.frame_done != 0u, PK_EV_FRAME, 0u);
         PK_ITER(env, ev);
         if (s.frame_done) {
             s.frame_done = 0;
