@@ -219,7 +219,8 @@ void export_v9(const Template& tp, const uint32_t* regs, const uint8_t* mem, con
 struct pk_handle {
     int device = 0;
     uint32_t n = 0, npad = 0, ngroups = 0;
-    uint32_t wave_lanes = 64;
+    uint32_t wave_lanes = 64;  // envs per wave in K1 (see pk_create)
+    uint32_t simds = 1024;     // SIMDs of the device (4 per CU)
     uint32_t frames = 24, release = 8, flags = 0, max_steps = 20480;
     uint32_t mbc = 3, bank_mask = 0;
     uint8_t* mem = nullptr;
@@ -307,10 +308,18 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     h->n = cfg->n_envs;
     h->npad = (cfg->n_envs + PK_LANES - 1) / PK_LANES * PK_LANES;
     h->ngroups = h->npad / PK_LANES;
-    if (const char* wl = getenv("PK_WAVE_LANES")) {
-        int v = atoi(wl);
-        if (v != 64 && v != 32 && v != 16) return fail(-EINVAL, "PK_WAVE_LANES must be 64, 32 or 16");
-        h->wave_lanes = (uint32_t)v;
+    {
+        // K1 wave shape: 32 envs per wave while that still fits two waves per SIMD (shorter,
+        // less divergent waves; the SIMD interleaves two of them), else 64.  PK_WAVE_LANES overrides.
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device) != hipSuccess || ncu <= 0) ncu = 256;
+        h->simds = 4u * (uint32_t)ncu;
+        h->wave_lanes = (h->npad / 32u <= 2u * h->simds) ? 32u : 64u;
+        if (const char* wl = getenv("PK_WAVE_LANES")) {
+            int v = atoi(wl);
+            if (v != 64 && v != 32 && v != 16) { delete h; return fail(-EINVAL, "PK_WAVE_LANES must be 64, 32 or 16"); }
+            h->wave_lanes = (uint32_t)v;
+        }
     }
     h->frames = cfg->frame_skip;
     h->release = cfg->release_frame;
@@ -480,6 +489,7 @@ int pk_step(pk_handle* h, const uint8_t* actions, uint8_t* screen_out, double* r
     a.lat_stride = (uint32_t)h->lat_stride;
     a.nslots = h->nslots; a.bank_slot = h->bank_slot; a.slot_bank = h->slot_bank;
     a.wave_lanes = h->wave_lanes;
+    a.simds = h->simds;
     int rc;
     if (h->prof && (rc = prof_event(h, s))) return rc;
     HIPCHK(pk_launch_step(a, s));

@@ -83,6 +83,7 @@ struct PkStepArgs {
     const int8_t* bank_slot;  // [128] LDS slot of each ROM bank, -1 = not staged
     const uint8_t* slot_bank; // [PK_LDS_SLOTS] bank held by each slot
     uint32_t wave_lanes;      // envs per 64-lane wave in K1 (64, 32 or 16): fewer lanes = more waves/SIMD
+    uint32_t simds;           // SIMDs of the device: K1 uses 256-thread workgroups while waves <= simds
 };
 
 struct PkResetArgs {

@@ -616,9 +616,11 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
 }
 
 hipError_t pk_launch_step(const PkStepArgs& a, hipStream_t s) {
+    // one wave per SIMD while the waves fit, else 512-thread workgroups put two waves on each SIMD
+    // of a CU (the ~115 KB of LDS staging allows one workgroup per CU)
     const u32 wl = a.wave_lanes;
-    const u32 block = wl >= 64u ? 256u : 512u;
     const u32 threads = a.npad * (PK_LANES / wl);
+    const u32 block = threads / PK_LANES <= a.simds ? 256u : 512u;
     const u32 grid = (threads + block - 1) / block;
     hipLaunchKernelGGL(pk_step_kernel, dim3(grid), dim3(block), 0, s, a);
     return hipGetLastError();

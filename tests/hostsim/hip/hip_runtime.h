@@ -72,6 +72,8 @@ static inline const char* hipGetErrorString(hipError_t) { return "hostsim error"
 static inline hipError_t hipGetLastError() { return hipSuccess; }
 static inline hipError_t hipSetDevice(int) { return hipSuccess; }
 static inline hipError_t hipDeviceSynchronize() { return hipSuccess; }
+enum hipDeviceAttribute_t { hipDeviceAttributeMultiprocessorCount = 1 };
+static inline hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t, int) { *v = 256; return hipSuccess; }
 static inline hipError_t hipMalloc(void** p, size_t n) {
     *p = aligned_alloc(256, (n + 255) / 256 * 256);
     return *p ? hipSuccess : hipErrorOutOfMemory;
