@@ -14,8 +14,11 @@
 //     has only single-level `if`s without `else`: LLVM's structurizer turns else-if chains into
 //     exec-mask bookkeeping that spilled SGPRs into VGPR lanes (measured: ~450 VALU per iteration).
 //   * paths a lane takes rarely (code outside the staged ROM, IO registers, MBC, OAM DMA, SRAM,
-//     deferred-line flush) are __noinline__ functions working on a copy of the lane state, so
-//     their code and registers stay out of the loop.
+//     deferred-line flush) sit in their own single-level `if`s and work on a copy of the lane
+//     state.  (Out-of-line calls were tried: the call convention moved the loop's uniform pointers
+//     into callee-saved VGPRs and turned the hot RAM accesses into flat loads — slower.)
+//   * a halted CPU that nothing can wake before VBlank jumps there in one iteration (HALT
+//     skip-ahead below) instead of one iteration per LCD mode event.
 //   * ROM bank 0 + the hottest switchable banks and the microcode table live in LDS; the RAM
 //     images are lane-interleaved in HBM (pk_layout.h) so lanes at the same guest address coalesce.
 #include <hip/hip_runtime.h>
@@ -243,7 +246,7 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
     st_img(c, fast_phys(a), v);
 }
 
-// ---- out-of-line rare paths (operate on a copy of the lane state) ----
+// ---- rare paths (operate on a copy of the lane state) ----
 __device__ __forceinline__ u32 pk_fetch_slow(const PkStepArgs* A, u8* g, u32 lane, const St* sp, u32 pc) {
     Ctx c;
     c.A = A; c.g = g; c.lane = lane; c.env = 0; c.gid = 0;
@@ -360,10 +363,18 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
         const bool flds = rom_staged(s, pc) && (pc & 0x3FFFu) < 0x3FFEu;
         const u32 la = sel(flds, rom_lds_index(s, pc), 0u);
         u32 bytes = __builtin_amdgcn_alignbyte(romw[(la >> 2) + 1u], romw[la >> 2], la & 3u);
-        if (exec && !flds) {
+        // code in RAM (e.g. the HRAM OAM-DMA wait loop): three image loads when pc..pc+2 stay in
+        // one 512-byte block of plain RAM
+        const bool fram = exec && !flds && fast_ram(pc) && fast_ram((pc + 2u) & 0xFFFFu) && ((pc ^ (pc + 2u)) & 0xFE00u) == 0u;
+        if (fram) {
+            const u32 p = fast_phys(pc);
+            bytes = ld_img(c, p) | (ld_img(c, p + 1u) << 8) | (ld_img(c, p + 2u) << 16);
+            ev |= PK_EV_F_BUS | sel(pc >= 0xFF80u, PK_EV_HRAM, 0u);
+        }
+        if (exec && !flds && !fram) {
             const St t = s;
             bytes = pk_fetch_slow(&A, c.g, c.lane, &t, pc);
-            ev |= PK_EV_F_BUS | sel(pc >= 0xFF80u, PK_EV_HRAM, 0u);
+            ev |= PK_EV_F_ROM16;
         }
         const u32 op = bytes & 0xFFu;
         // INT pseudo-op: the vector rides in imm16
@@ -405,12 +416,17 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
             m0 = lds_rom[rom_lds_index(s, addr0)];
             m1 = sel(rd2, (u32)lds_rom[rom_lds_index(s, addr1)], 0u);
         }
-        if (rd && !rram && !rrom) {
+        const bool rio = rd && !rd2 && addr0 >= 0xFF00u && (addr0 < 0xFF80u || addr0 == 0xFFFFu);
+        if (rio) {  // IO register (LY, STAT, joypad, ...)
+            m0 = io_read(c, s, addr0);
+            ev |= PK_EV_RD_IO;
+        }
+        if (rd && !rram && !rrom && !rio) {
             const St t = s;
             const u32 m = pk_read_slow(&A, c.g, c.lane, &t, addr0, addr1, rd2 ? 1u : 0u);
             m0 = m & 0xFFu;
             m1 = m >> 8;
-            ev |= PK_EV_RD_IO;
+            ev |= PK_EV_RD_ROMG;
         }
         ev |= sel(rd, PK_EV_RD | sel(rd2, PK_EV_RD2, 0u) | sel(rram, PK_EV_RD_RAM, 0u) | sel(rrom, PK_EV_RD_ROMLDS, 0u)
                       | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
@@ -507,6 +523,31 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
         // ---------------- HALT fast-forward, timer, LCD (pyboy mb.tick) ----------------
         const u32 tac = s.tim0 >> 24;
         const u32 dsh = sel((tac & 3u) == 0u, 10u, sel((tac & 3u) == 1u, 4u, sel((tac & 3u) == 2u, 6u, 8u)));
+        // HALT skip-ahead: a halted CPU that nothing can wake before VBlank (no pending or queued
+        // interrupt, timer off, STAT HBlank/OAM/LYC interrupts off, frame not rendered) would spend
+        // one loop iteration per LCD mode event (3 per scanline) fast-forwarding to it.  Jump to
+        // the state right after line 143's mode-0 event in one step instead (exactly the state those
+        // iterations would reach: LY, STAT mode and coincidence bit, clock, DIV, watchdog budget),
+        // so the VBlank event itself is processed below as usual.
+        {
+            const u32 cpu = s.cpu, stat = bfe8(s.lcd0, 8), ly = bfe8(s.lcd0, 16), nm = s.lcd2 >> 24;
+            const bool cand = (cpu & (CPU_HALT | CPU_QUEUED)) == CPU_HALT && ((cpu >> 8) & (cpu >> 16) & 0x1Fu) == 0u
+                           && (s.lcd0 & 0x80u) && (stat & 0x68u) == 0u && !(tac & 4u) && !s.render && ly < 143u && nm != 1u && s.clock <= s.target;
+            const u32 lines = 143u - ly;
+            const u32 vbl = sel(nm == 2u, s.target + 456u * lines, s.target - sel(nm == 3u, 80u, 250u) + 456u * (lines + 1u));
+            const u32 nev = sel(nm == 3u, 2u, sel(nm == 0u, 1u, 0u)) + 3u * lines + 1u;  // iterations up to VBlank
+            const u32 tnew = vbl - 206u;                                                  // line 143 mode-0 event
+            if (cand && budget + (vbl - s.clock) + nev <= 16u * FRAME_CYCLES) {
+                const u32 skipped = tnew - s.clock;
+                s.divacc = (s.divacc + skipped) & 0xFFFFu;
+                budget += skipped + (nev - 1u);
+                s.clock = tnew;
+                s.target = vbl;
+                const u32 st2 = (stat & 0xF8u) | sel((s.lcd0 >> 24) == 143u, 4u, 0u);
+                s.lcd0 = (s.lcd0 & 0xFF0000FFu) | (st2 << 8) | (143u << 16);
+                s.lcd2 = (s.lcd2 & 0x00FFFFFFu) | (1u << 24);
+            }
+        }
         if (s.cpu & CPU_HALT) {
             const int tb = (int)sel(tac & 4u, ((0x100u - bfe8(s.tim0, 8)) << dsh) - s.timac, 1u << 16);
             const int ta = (int)s.target - (int)s.clock;
