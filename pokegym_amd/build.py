@@ -35,7 +35,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     for src in SOURCES:
         obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + ".o")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-               "-Wno-unused-function", "-c", "-o", obj]
+               "-Wno-unused-function", "-Wno-bitwise-instead-of-logical", "-c", "-o", obj]
         if src.endswith(".cpp"):
             cmd += ["-x", "hip"]
         cmd.append(os.path.join(CSRC, src))
