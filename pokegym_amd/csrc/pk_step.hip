@@ -346,18 +346,23 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
     while (frame < A.frames) {
         u32 ev = 0;
         // ---------------- front-end: cpu.tick / check_interrupts ----------------
+        // common case (running, nothing pending): execute at pc; otherwise the full PyBoy order
         const u32 cpu0 = s.cpu;
         const u32 pend = (cpu0 >> 8) & (cpu0 >> 16) & 0x1Fu;
-        const bool crashed = (cpu0 & CPU_CRASH) != 0u;
-        const bool halted = (cpu0 & CPU_HALT) != 0u;
-        const bool queued = (cpu0 & CPU_QUEUED) != 0u;
-        const bool doint = !crashed && !queued && pend != 0u;
-        const bool dispatch = doint && (cpu0 & CPU_IME) != 0u;
-        const bool wake = !crashed && !doint && halted && queued;
-        const bool exec = !crashed && !doint && (!halted || queued);
-        const u32 pc = (s.pc + sel((doint && halted) || wake, 1u, 0u)) & 0xFFFFu;
-        const u32 intflag = pend & (0u - pend);
-        s.cpu = sel(doint, (cpu0 | CPU_QUEUED) & ~CPU_HALT, sel(wake, cpu0 & ~CPU_HALT, cpu0)) ^ sel(dispatch, intflag << 16, 0u);
+        bool exec = true, doint = false, dispatch = false;
+        u32 pc = s.pc, intflag = 0;
+        if ((cpu0 & (CPU_CRASH | CPU_HALT | CPU_QUEUED)) | pend) {
+            const bool crashed = (cpu0 & CPU_CRASH) != 0u;
+            const bool halted = (cpu0 & CPU_HALT) != 0u;
+            const bool queued = (cpu0 & CPU_QUEUED) != 0u;
+            doint = !crashed && !queued && pend != 0u;
+            dispatch = doint && (cpu0 & CPU_IME) != 0u;
+            const bool wake = !crashed && !doint && halted && queued;
+            exec = !crashed && !doint && (!halted || queued);
+            pc = (pc + sel((doint && halted) || wake, 1u, 0u)) & 0xFFFFu;
+            intflag = pend & (0u - pend);
+            s.cpu = sel(doint, (cpu0 | CPU_QUEUED) & ~CPU_HALT, sel(wake, cpu0 & ~CPU_HALT, cpu0)) ^ sel(dispatch, intflag << 16, 0u);
+        }
 
         // ---------------- fetch: LDS-staged ROM for every lane; other code out of line ----------------
         const bool flds = rom_staged(s, pc) && (pc & 0x3FFFu) < 0x3FFEu;
@@ -385,8 +390,9 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
         ev |= sel(exec, PK_EV_EXEC | sel(flds, PK_EV_F_LDS, 0u) | sel(op == 0xCBu, PK_EV_CB, 0u), 0u)
             | sel(dispatch, PK_EV_INT, 0u) | sel(!exec && !dispatch, PK_EV_IDLE, 0u);
         if (exec) PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, op);
-        const uint4 e0 = ucv[di * 2u], e1 = ucv[di * 2u + 1u];
-        const u32 D = e0.x, U = e0.y, PX = e0.z, PY = e0.w, S0 = e1.x, S1 = e1.y, PA = e1.z, K = e1.w;
+        const uint4 e0 = ucv[di * 3u], e1 = ucv[di * 3u + 1u], e2 = ucv[di * 3u + 2u];
+        const u32 D = e0.x, U = e0.y, K = e0.z, XR = e1.x, XE = e1.y, YR = e1.z, YE = e1.w, AR = e2.x, AE = e2.y,
+                  S0 = e2.z, S1 = e2.w;
 
         // ---------------- operands, condition, memory address ----------------
         const u32 w0 = s.w0, w1 = s.w1, sp = s.sp;
@@ -397,9 +403,8 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
         const u32 hl = w1 & 0xFFFFu;
         const u32 pcn = (pc + (D & 3u)) & 0xFFFFu;
         const u32 taken = (((F | 0x100u) >> ((D >> PK_DB_CPOS) & 15u)) & 1u) ^ bit(D, PK_DB_CINV);
-        const u32 abase = perm(w1, w0, PA);
-        const u32 aim = sel(bit(D, PK_DB_AHN), 0xFF00u | b1, imm16);
-        const u32 asrc = sel(bit(D, PK_DB_ASP), sp, sel(bit(D, PK_DB_AIMM), aim, abase));
+        // operand pools: registers (w1:w0) and ext (q1:q0) = instruction bytes, m0|m1 and SP
+        const u32 asrc = perm(w1, w0, AR) | perm(sp << 16, bytes, AE);
         const u32 addr0 = (asrc + (u32)sfield(D, PK_DB_AOFF, 2)) & 0xFFFFu;
         const u32 addr1 = (addr0 + (u32)sfield(D, PK_DB_ADIR, 2)) & 0xFFFFu;
 
@@ -434,11 +439,10 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
         const u32 m16 = m0 | (m1 << 8);
 
         // ---------------- fused datapath ----------------
-        const u32 X = sel(bit(U, PK_UB_XSP), sp, sel(bit(U, PK_UB_XMEM), m0, perm(w1, w0, PX)));
+        const u32 q1 = m16 | (sp << 16);
+        const u32 X = perm(w1, w0, XR) | perm(q1, bytes, XE);
+        const u32 Y = perm(w1, w0, YR) | perm(q1, bytes, YE) | (K & 0xFFu);
         const u32 sx8 = (u32)(int)(int8_t)(u8)b1 & 0xFFFFu;
-        const u32 imm = sel(bit(U, PK_UB_SEXT), sx8, sel(bit(U, PK_UB_IMM8), b1, imm16));
-        const u32 Y = sel(bit(U, PK_UB_YIMM), imm, sel(bit(U, PK_UB_YMEM), m16, sel(bit(D, PK_DB_YSP), sp, perm(w1, w0, PY))))
-                    | (K & 0xFFu);
         // adder: r = X + (sub ? ~Y : Y) + cin; carries into each bit = X ^ Y' ^ r
         const u32 sub = bit(U, PK_UB_SUB);
         const u32 Yx = Y ^ ((0u - sub) & 0xFFFFu);

@@ -1,8 +1,10 @@
 // pk_ucode.h — SM83 microcode for the K1 step kernel (pk_step.hip), built on the host and staged
-// in LDS.  One 32-byte entry per opcode (256 base + 256 CB-prefixed + 3 pseudo-ops) drives ONE
+// in LDS.  One 48-byte entry per opcode (256 base + 256 CB-prefixed + 3 pseudo-ops) drives ONE
 // fused datapath that every lane runs each iteration, whatever opcode it holds:
 //
-//   X = SP | m0 | perm(w1:w0, PX)          Y = (imm | m16 | SP | perm(w1:w0, PY)) | yconst
+//   X = perm(w1:w0, XR) | perm(ext, XE)     Y = perm(w1:w0, YR) | perm(ext, YE) | yconst
+//   (ext = the instruction bytes op|n|n2 and m0|m1|SP: immediates, memory operands, SP and the
+//   sign of n all come out of one v_perm with a per-opcode selector)
 //   adder  r = X + (sub ? ~Y : Y) + cin;   carries = X ^ Y' ^ r  ->  H, C at bit 4/8 or 12/16
 //   logic  X & Y | X ^ Y | X | Y           rotate/shift unit on X
 //   val    = res16 | F' << 16 | res8 << 24;  w0 = perm(val, w0, S0);  w1 = perm(val, w1, S1)
@@ -16,8 +18,9 @@
 #pragma once
 #include <stdint.h>
 
-// ---- entry layout: 8 dwords ----
-enum { PK_UE_D = 0, PK_UE_U, PK_UE_PX, PK_UE_PY, PK_UE_S0, PK_UE_S1, PK_UE_PA, PK_UE_K, PK_UE_WORDS };
+// ---- entry layout: 12 dwords (three ds_read_b128) ----
+enum { PK_UE_D = 0, PK_UE_U, PK_UE_K, PK_UE_PAD, PK_UE_XR, PK_UE_XE, PK_UE_YR, PK_UE_YE, PK_UE_AR, PK_UE_AE,
+       PK_UE_S0, PK_UE_S1, PK_UE_WORDS };
 #define PK_UC_ENTRIES 515u
 #define PK_UC_INT 512u    // pseudo-op: interrupt dispatch (push PC, jump to the vector)
 #define PK_UC_IDLE 513u   // pseudo-op: halted / crashed CPU, 4 cycles
@@ -29,9 +32,9 @@ enum { PK_UE_D = 0, PK_UE_U, PK_UE_PX, PK_UE_PY, PK_UE_S0, PK_UE_S1, PK_UE_PA, P
 #define PK_DB_RD2 3       // read m1 at addr1
 #define PK_DB_WR 4        // write wv0 at addr0
 #define PK_DB_WR2 5       // write wv1 at addr1
-#define PK_DB_ASP 6       // address source SP
-#define PK_DB_AIMM 7      // address source immediate
-#define PK_DB_AHN 8       // immediate address is 0xFF00|n
+#define PK_DB_ASP 6       // (builder only) address source SP        -> AE selector
+#define PK_DB_AIMM 7      // (builder only) address source immediate -> AE selector
+#define PK_DB_AHN 8       // (builder only) immediate address 0xFF00|n
 #define PK_DB_AOFF 9      // 2 bits signed: addr0 = src + aoff
 #define PK_DB_ADIR 11     // 2 bits signed: addr1 = addr0 + adir
 #define PK_DB_CYC 13      // 3 bits cycles/4
@@ -43,10 +46,11 @@ enum { PK_UE_D = 0, PK_UE_U, PK_UE_PX, PK_UE_PY, PK_UE_S0, PK_UE_S1, PK_UE_PA, P
 #define PK_DB_HALT 28     // set HALT
 #define PK_DB_CRASH 29    // set CRASH|HALT (illegal opcode)
 #define PK_DB_DAA 30      // DAA (rare path)
-#define PK_DB_YSP 31      // Y = SP
+#define PK_DB_YSP 31      // (builder only) Y = SP
 enum { PK_T_NONE = 0, PK_T_IMM, PK_T_HL, PK_T_JR, PK_T_M16, PK_T_RST };
 
 // U word: datapath
+// bits 0-5 are builder-only operand flags, turned into the XE/YE selectors by pk_build_ucode
 #define PK_UB_XSP 0       // X = SP
 #define PK_UB_XMEM 1      // X = m0
 #define PK_UB_YIMM 2      // Y = immediate
@@ -80,6 +84,15 @@ enum { PK_T_NONE = 0, PK_T_IMM, PK_T_HL, PK_T_JR, PK_T_M16, PK_T_RST };
 
 // perm selectors over (w1:w0) = bytes C B E D L H F A ; 0x0C = 0x00, 0x0D = 0xFF
 #define PK_PZERO 0x0C0C0C0Cu
+// perm selectors over the ext pool (q1:q0): q0 = op | n<<8 | n2<<16, q1 = m0 | m1<<8 | SP<<16;
+// 0x08 = the sign of n replicated
+#define PK_E_SP 0x0C0C0706u
+#define PK_E_M0 0x0C0C0C04u
+#define PK_E_M16 0x0C0C0504u
+#define PK_E_N 0x0C0C0C01u
+#define PK_E_NN 0x0C0C0201u
+#define PK_E_SEXTN 0x0C0C0801u
+#define PK_E_HN 0x0C0C0D01u
 
 static inline uint32_t pk_r8_byte(int r) {  // SM83 r8 index (B C D E H L (HL) A) -> byte in w1:w0
     static const uint8_t b[8] = {1, 0, 3, 2, 5, 4, 0xFF, 7};
@@ -396,13 +409,35 @@ static inline PkUop pk_uop_cb(int op) {
 }
 
 // the whole table: [0,256) base, [256,512) CB-prefixed, then the three pseudo-ops
-static inline void pk_build_ucode(uint32_t* t /* PK_UC_ENTRIES * 8 */) {
+static inline void pk_store_uop(uint32_t* e, PkUop o) {
+    // operand sources -> ext-pool selectors (the register-pool selector is zeroed when unused)
+    uint32_t xe = PK_PZERO, ye = PK_PZERO, ae = PK_PZERO;
+    if (o.u & pk_fld(1, PK_UB_XSP)) xe = PK_E_SP;
+    else if (o.u & pk_fld(1, PK_UB_XMEM)) xe = PK_E_M0;
+    if (o.u & pk_fld(1, PK_UB_YIMM)) ye = (o.u & pk_fld(1, PK_UB_SEXT)) ? PK_E_SEXTN : (o.u & pk_fld(1, PK_UB_IMM8)) ? PK_E_N : PK_E_NN;
+    else if (o.u & pk_fld(1, PK_UB_YMEM)) ye = PK_E_M16;
+    else if (o.d & pk_fld(1, PK_DB_YSP)) ye = PK_E_SP;
+    if (o.d & pk_fld(1, PK_DB_ASP)) ae = PK_E_SP;
+    else if (o.d & pk_fld(1, PK_DB_AIMM)) ae = (o.d & pk_fld(1, PK_DB_AHN)) ? PK_E_HN : PK_E_NN;
+    e[PK_UE_D] = o.d & ~(pk_fld(1, PK_DB_ASP) | pk_fld(1, PK_DB_AIMM) | pk_fld(1, PK_DB_AHN) | pk_fld(1, PK_DB_YSP));
+    e[PK_UE_U] = o.u & ~63u;
+    e[PK_UE_K] = o.k;
+    e[PK_UE_PAD] = 0;
+    e[PK_UE_XR] = xe != PK_PZERO ? PK_PZERO : o.px;
+    e[PK_UE_XE] = xe;
+    e[PK_UE_YR] = ye != PK_PZERO ? PK_PZERO : o.py;
+    e[PK_UE_YE] = ye;
+    e[PK_UE_AR] = ae != PK_PZERO ? PK_PZERO : o.pa;
+    e[PK_UE_AE] = ae;
+    e[PK_UE_S0] = o.s0;
+    e[PK_UE_S1] = o.s1;
+}
+
+static inline void pk_build_ucode(uint32_t* t /* PK_UC_ENTRIES * PK_UE_WORDS */) {
     for (int i = 0; i < 512; i++) {
         PkUop o = i < 256 ? pk_uop(i) : pk_uop_cb(i - 256);
         if (i == 0xCB) o = pk_uop_base(2, 8);  // never executed: the kernel indexes 256 + second byte
-        uint32_t* e = t + (size_t)i * PK_UE_WORDS;
-        e[PK_UE_D] = o.d; e[PK_UE_U] = o.u; e[PK_UE_PX] = o.px; e[PK_UE_PY] = o.py;
-        e[PK_UE_S0] = o.s0; e[PK_UE_S1] = o.s1; e[PK_UE_PA] = o.pa; e[PK_UE_K] = o.k;
+        pk_store_uop(t + (size_t)i * PK_UE_WORDS, o);
     }
     // INT: push PC (len 0: the current PC), jump to the vector the front-end puts in imm16, IME off
     PkUop it = pk_uop_base(0, 0);
@@ -411,10 +446,5 @@ static inline void pk_build_ucode(uint32_t* t /* PK_UC_ENTRIES * 8 */) {
     it.u |= pk_fld(1, PK_UB_W16) | pk_fld(1, PK_UB_WPC) | pk_sfld(-2, PK_UB_SPD, 3);
     PkUop idle = pk_uop_base(0, 4), nop0 = pk_uop_base(0, 0);
     const PkUop ps[3] = {it, idle, nop0};
-    for (int j = 0; j < 3; j++) {
-        uint32_t* e = t + (size_t)(512 + j) * PK_UE_WORDS;
-        const PkUop& o = ps[j];
-        e[PK_UE_D] = o.d; e[PK_UE_U] = o.u; e[PK_UE_PX] = o.px; e[PK_UE_PY] = o.py;
-        e[PK_UE_S0] = o.s0; e[PK_UE_S1] = o.s1; e[PK_UE_PA] = o.pa; e[PK_UE_K] = o.k;
-    }
+    for (int j = 0; j < 3; j++) pk_store_uop(t + (size_t)(512 + j) * PK_UE_WORDS, ps[j]);
 }

@@ -25,8 +25,8 @@
 #define __noinline__ __attribute__((noinline))
 #define __launch_bounds__(...)
 #define __builtin_amdgcn_readfirstlane(x) (x)
-// v_perm_b32: byte i of the result = byte sel.byte[i] of {hi, lo} (0-3 lo, 4-7 hi), 0x0C -> 0x00,
-// >= 0x0D -> 0xFF (8-11: sign replication, unused by the kernels)
+// v_perm_b32: byte i of the result = byte sel.byte[i] of {hi, lo} (0-3 lo, 4-7 hi), 8-11 the sign
+// bit of lo[15], lo[31], hi[15], hi[31] replicated, 0x0C -> 0x00, >= 0x0D -> 0xFF
 static inline uint32_t __builtin_amdgcn_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
     uint64_t v = ((uint64_t)hi << 32) | lo;
     uint32_t r = 0;
@@ -35,7 +35,10 @@ static inline uint32_t __builtin_amdgcn_perm(uint32_t hi, uint32_t lo, uint32_t 
         if (s < 8) b = (uint32_t)(v >> (8 * s)) & 0xFFu;
         else if (s == 0x0C) b = 0;
         else if (s > 0x0C) b = 0xFF;
-        else abort();
+        else {  // 8..11: replicate the sign bit of lo[15], lo[31], hi[15], hi[31]
+            static const int bitpos[4] = {15, 31, 47, 63};
+            b = ((v >> bitpos[s - 8]) & 1u) ? 0xFFu : 0u;
+        }
         r |= b << (8 * i);
     }
     return r;
