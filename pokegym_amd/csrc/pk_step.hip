@@ -397,7 +397,6 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
         // ---------------- operands, condition, memory address ----------------
         const u32 w0 = s.w0, w1 = s.w1, sp = s.sp;
         const u32 b1 = (bytes >> 8) & 0xFFu;
-        const u32 imm16 = (bytes >> 8) & 0xFFFFu;
         const u32 F = (w1 >> 16) & 0xFFu;
         const u32 fc = (F >> 4) & 1u;
         const u32 hl = w1 & 0xFFFFu;
@@ -488,7 +487,7 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
         // ---------------- control transfer, SP, IME/HALT ----------------
         const u32 tsrc = (D >> PK_DB_TSRC) & 7u;
         const u32 jrt = (pc + 2u + sx8) & 0xFFFFu;
-        const u32 tgt = sel(tsrc == PK_T_IMM, imm16, sel(tsrc == PK_T_HL, hl, sel(tsrc == PK_T_JR, jrt, sel(tsrc == PK_T_M16, m16, bytes & 0x38u))));
+        const u32 tgt = sel(tsrc == PK_J_JR, jrt, (X | Y) & 0xFFFFu);  // JP/CALL/INT nn, JP HL, RET, RST: X | Y
         const bool jump = tsrc != 0u && taken != 0u;
         s.pc = sel(jump, tgt, pcn);
         ev |= sel(jump, PK_EV_JUMP, 0u);
@@ -496,11 +495,8 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
         const u32 sp2 = (sp + ((u32)sfield(U, PK_UB_SPD, 3) & (0u - taken))) & 0xFFFFu;
         s.sp = sel(bit(U, PK_UB_SPW), res16, sp2);
         {
-            const u32 ime = (D >> PK_DB_IME) & 3u;
-            u32 cpu = s.cpu;
-            cpu = sel(ime == 1u, cpu & ~CPU_IME, sel(ime == 2u, cpu | CPU_IME, cpu));
-            cpu |= (bit(D, PK_DB_HALT) * CPU_HALT) | (bit(D, PK_DB_CRASH) * (CPU_CRASH | CPU_HALT));
-            s.cpu = sel(exec, cpu & ~CPU_QUEUED, cpu);
+            // IME / HALT / CRASH / QUEUED: (cpu & keep) | set from the microcode
+            s.cpu = (s.cpu & (0xFFFFFFF0u | ((K >> PK_KB_CPUAND) & 15u))) | (K >> PK_KB_CPUOR);
         }
 
         // ---------------- memory writes (wv0 at addr0, wv1 at addr1) ----------------

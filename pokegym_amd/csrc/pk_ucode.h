@@ -41,13 +41,14 @@ enum { PK_UE_D = 0, PK_UE_U, PK_UE_K, PK_UE_PAD, PK_UE_XR, PK_UE_XE, PK_UE_YR, P
 #define PK_DB_XCYC 16     // 2 bits extra cycles/4 when the condition holds
 #define PK_DB_CPOS 18     // 4 bits: condition = bit cpos of (F | 0x100)
 #define PK_DB_CINV 22     //         ^ cinv
-#define PK_DB_TSRC 23     // 3 bits jump target: 0 none 1 imm16 2 HL 3 JR 4 m16 5 RST
+#define PK_DB_TSRC 23     // 3 bits jump target (builder: PK_T_*; stored: 0 none, 1 X|Y, 2 JR)
 #define PK_DB_IME 26      // 2 bits: 0 keep 1 clear 2 set
 #define PK_DB_HALT 28     // set HALT
 #define PK_DB_CRASH 29    // set CRASH|HALT (illegal opcode)
 #define PK_DB_DAA 30      // DAA (rare path)
 #define PK_DB_YSP 31      // (builder only) Y = SP
 enum { PK_T_NONE = 0, PK_T_IMM, PK_T_HL, PK_T_JR, PK_T_M16, PK_T_RST };
+enum { PK_J_NONE = 0, PK_J_XY = 1, PK_J_JR = 2 };  // stored: target = X | Y (operands chosen below) or pc+2+e
 
 // U word: datapath
 // bits 0-5 are builder-only operand flags, turned into the XE/YE selectors by pk_build_ucode
@@ -81,6 +82,8 @@ enum { PK_T_NONE = 0, PK_T_IMM, PK_T_HL, PK_T_JR, PK_T_M16, PK_T_RST };
 #define PK_KB_YCONST 0    // 8 bits ORed into Y
 #define PK_KB_FKEEP 8     // 8 bits: F bits kept
 #define PK_KB_FCONST 16   // 8 bits: F bits set
+#define PK_KB_CPUAND 24   // 4 bits: CPU state bits (IME HALT QUEUED CRASH) kept
+#define PK_KB_CPUOR 28    // 4 bits: CPU state bits set
 
 // perm selectors over (w1:w0) = bytes C B E D L H F A ; 0x0C = 0x00, 0x0D = 0xFF
 #define PK_PZERO 0x0C0C0C0Cu
@@ -347,6 +350,7 @@ static inline PkUop pk_uop(int op) {
         }
         if ((op & 7) == 7) {  // RST
             o = pk_uop_base(1, 16);
+            o.k |= pk_fld((uint32_t)op & 0x38u, PK_KB_YCONST);  // vector rides in Y
             o.d |= pk_fld(PK_T_RST, PK_DB_TSRC) | pk_fld(1, PK_DB_WR) | pk_fld(1, PK_DB_WR2) | pk_fld(1, PK_DB_ASP)
                  | pk_sfld(-1, PK_DB_AOFF, 2) | pk_sfld(-1, PK_DB_ADIR, 2);
             o.u |= pk_fld(1, PK_UB_W16) | pk_fld(1, PK_UB_WPC) | pk_sfld(-2, PK_UB_SPD, 3);
@@ -409,7 +413,35 @@ static inline PkUop pk_uop_cb(int op) {
 }
 
 // the whole table: [0,256) base, [256,512) CB-prefixed, then the three pseudo-ops
-static inline void pk_store_uop(uint32_t* e, PkUop o) {
+static inline void pk_store_uop(uint32_t* e, PkUop o, bool real) {
+    // CPU state update as (cpu & keep) | set: IME from DI/EI/RETI/INT, HALT, CRASH; an executed
+    // instruction clears QUEUED (pyboy cpu.tick), the pseudo-ops keep it
+    {
+        const uint32_t ime = (o.d >> PK_DB_IME) & 3u;
+        uint32_t keep = 0xFu, set = 0u;
+        if (real) keep &= ~4u;
+        if (ime == 1u) keep &= ~1u;
+        if (ime == 2u) set |= 1u;
+        if (o.d & pk_fld(1, PK_DB_HALT)) set |= 2u;
+        if (o.d & pk_fld(1, PK_DB_CRASH)) set |= 2u | 8u;
+        o.k |= pk_fld(keep, PK_KB_CPUAND) | pk_fld(set, PK_KB_CPUOR);
+    }
+    // jump targets through the operand pools: JP/CALL/INT nn -> Y = nn, JP HL -> X = HL,
+    // RET -> Y = m16, RST -> Y = yconst (the vector); the datapath result of these ops is unused
+    const uint32_t ts = (o.d >> PK_DB_TSRC) & 7u;
+    uint32_t js = PK_J_NONE;
+    if (ts == PK_T_JR) js = PK_J_JR;
+    else if (ts != PK_T_NONE) {
+        js = PK_J_XY;
+        o.u &= ~(pk_fld(1, PK_UB_XSP) | pk_fld(1, PK_UB_XMEM) | pk_fld(1, PK_UB_YIMM) | pk_fld(1, PK_UB_IMM8) |
+                 pk_fld(1, PK_UB_SEXT) | pk_fld(1, PK_UB_YMEM));
+        o.px = PK_PZERO;
+        o.py = PK_PZERO;
+        if (ts == PK_T_IMM) o.u |= pk_fld(1, PK_UB_YIMM);
+        if (ts == PK_T_HL) o.px = pk_sel16(2);
+        if (ts == PK_T_M16) o.u |= pk_fld(1, PK_UB_YMEM);
+    }
+    o.d = (o.d & ~(7u << PK_DB_TSRC)) | pk_fld(js, PK_DB_TSRC);
     // operand sources -> ext-pool selectors (the register-pool selector is zeroed when unused)
     uint32_t xe = PK_PZERO, ye = PK_PZERO, ae = PK_PZERO;
     if (o.u & pk_fld(1, PK_UB_XSP)) xe = PK_E_SP;
@@ -437,7 +469,7 @@ static inline void pk_build_ucode(uint32_t* t /* PK_UC_ENTRIES * PK_UE_WORDS */)
     for (int i = 0; i < 512; i++) {
         PkUop o = i < 256 ? pk_uop(i) : pk_uop_cb(i - 256);
         if (i == 0xCB) o = pk_uop_base(2, 8);  // never executed: the kernel indexes 256 + second byte
-        pk_store_uop(t + (size_t)i * PK_UE_WORDS, o);
+        pk_store_uop(t + (size_t)i * PK_UE_WORDS, o, true);
     }
     // INT: push PC (len 0: the current PC), jump to the vector the front-end puts in imm16, IME off
     PkUop it = pk_uop_base(0, 0);
@@ -446,5 +478,5 @@ static inline void pk_build_ucode(uint32_t* t /* PK_UC_ENTRIES * PK_UE_WORDS */)
     it.u |= pk_fld(1, PK_UB_W16) | pk_fld(1, PK_UB_WPC) | pk_sfld(-2, PK_UB_SPD, 3);
     PkUop idle = pk_uop_base(0, 4), nop0 = pk_uop_base(0, 0);
     const PkUop ps[3] = {it, idle, nop0};
-    for (int j = 0; j < 3; j++) pk_store_uop(t + (size_t)(512 + j) * PK_UE_WORDS, ps[j]);
+    for (int j = 0; j < 3; j++) pk_store_uop(t + (size_t)(512 + j) * PK_UE_WORDS, ps[j], false);
 }
