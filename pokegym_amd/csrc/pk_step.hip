@@ -368,18 +368,18 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
         const bool flds = rom_staged(s, pc) && (pc & 0x3FFFu) < 0x3FFEu;
         const u32 la = sel(flds, rom_lds_index(s, pc), 0u);
         u32 bytes = __builtin_amdgcn_alignbyte(romw[(la >> 2) + 1u], romw[la >> 2], la & 3u);
-        // code in RAM (e.g. the HRAM OAM-DMA wait loop): three image loads when pc..pc+2 stay in
-        // one 512-byte block of plain RAM
-        const bool fram = exec && !flds && fast_ram(pc) && fast_ram((pc + 2u) & 0xFFFFu) && ((pc ^ (pc + 2u)) & 0xFE00u) == 0u;
-        if (fram) {
-            const u32 p = fast_phys(pc);
-            bytes = ld_img(c, p) | (ld_img(c, p + 1u) << 8) | (ld_img(c, p + 2u) << 16);
-            ev |= PK_EV_F_BUS | sel(pc >= 0xFF80u, PK_EV_HRAM, 0u);
-        }
-        if (exec && !flds && !fram) {
-            const St t = s;
-            bytes = pk_fetch_slow(&A, c.g, c.lane, &t, pc);
-            ev |= PK_EV_F_ROM16;
+        // code outside the staged ROM (rare): RAM code such as the HRAM OAM-DMA wait loop reads the
+        // image (three loads when pc..pc+2 stay in one 512-byte block of plain RAM), else the bus
+        if (exec & !flds) {
+            if (fast_ram(pc) & fast_ram((pc + 2u) & 0xFFFFu) & (((pc ^ (pc + 2u)) & 0xFE00u) == 0u)) {
+                const u32 p = fast_phys(pc);
+                bytes = ld_img(c, p) | (ld_img(c, p + 1u) << 8) | (ld_img(c, p + 2u) << 16);
+                ev |= PK_EV_F_BUS | sel(pc >= 0xFF80u, PK_EV_HRAM, 0u);
+            } else {
+                const St t = s;
+                bytes = pk_fetch_slow(&A, c.g, c.lane, &t, pc);
+                ev |= PK_EV_F_ROM16;
+            }
         }
         const u32 op = bytes & 0xFFu;
         // INT pseudo-op: the vector rides in imm16
@@ -420,17 +420,17 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
             m0 = lds_rom[rom_lds_index(s, addr0)];
             m1 = sel(rd2, (u32)lds_rom[rom_lds_index(s, addr1)], 0u);
         }
-        const bool rio = rd && !rd2 && addr0 >= 0xFF00u && (addr0 < 0xFF80u || addr0 == 0xFFFFu);
-        if (rio) {  // IO register (LY, STAT, joypad, ...)
-            m0 = io_read(c, s, addr0);
-            ev |= PK_EV_RD_IO;
-        }
-        if (rd && !rram && !rrom && !rio) {
-            const St t = s;
-            const u32 m = pk_read_slow(&A, c.g, c.lane, &t, addr0, addr1, rd2 ? 1u : 0u);
-            m0 = m & 0xFFu;
-            m1 = m >> 8;
-            ev |= PK_EV_RD_ROMG;
+        if (rd & !rram & !rrom) {  // rare: IO registers (LY, STAT, joypad, ...), SRAM, unstaged ROM
+            if (!rd2 & (addr0 >= 0xFF00u) & ((addr0 < 0xFF80u) | (addr0 == 0xFFFFu))) {
+                m0 = io_read(c, s, addr0);
+                ev |= PK_EV_RD_IO;
+            } else {
+                const St t = s;
+                const u32 m = pk_read_slow(&A, c.g, c.lane, &t, addr0, addr1, rd2 ? 1u : 0u);
+                m0 = m & 0xFFu;
+                m1 = m >> 8;
+                ev |= PK_EV_RD_ROMG;
+            }
         }
         ev |= sel(rd, PK_EV_RD | sel(rd2, PK_EV_RD2, 0u) | sel(rram, PK_EV_RD_RAM, 0u) | sel(rrom, PK_EV_RD_ROMLDS, 0u)
                       | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
