@@ -409,8 +409,8 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
 
         // ---------------- memory reads (m0 at addr0, m1 at addr1) ----------------
         const bool rd = bit(D, PK_DB_RD) != 0u, rd2 = bit(D, PK_DB_RD2) != 0u;
-        const bool rram = rd && fast_ram(addr0) && fast_ram(addr1);  // addr1 == addr0 for 1-byte reads
-        const bool rrom = rd && rom_staged(s, addr0) && rom_staged(s, addr1);
+        const bool rram = rd & fast_ram(addr0) & fast_ram(addr1);  // addr1 == addr0 for 1-byte reads
+        const bool rrom = rd & rom_staged(s, addr0) & rom_staged(s, addr1);
         u32 m0 = 0, m1 = 0;
         if (rram) {
             m0 = ld_img(c, fast_phys(addr0));
@@ -505,17 +505,22 @@ __global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
         const u32 wv = sel(bit(U, PK_UB_W16), pushv, res8);
         const bool hifirst = bit(D, PK_DB_ADIR + 1) != 0u;  // adir = -1: push writes the high byte first
         const u32 wv0 = sel(hifirst, wv >> 8, wv) & 0xFFu, wv1 = sel(hifirst, wv, wv >> 8) & 0xFFu;
-        const bool wvo = s.npend != 0u && (vram_or_oam(addr0) || (wr2 && vram_or_oam(addr1)));
-        const bool wram = wr && fast_ram(addr0) && fast_ram(addr1) && !wvo;
+        const bool wram = wr & fast_ram(addr0) & fast_ram(addr1);
         if (wram) {
+            // VRAM / OAM change while rendered lines are pending: rasterise them first (rare)
+            if ((s.npend != 0u) & (vram_or_oam(addr0) | (wr2 & vram_or_oam(addr1)))) {
+                flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, env, c.gid);
+                s.npend = 0;
+                ev |= PK_EV_FLUSH;
+            }
             st_img(c, fast_phys(addr0), wv0);
             if (wr2) st_img(c, fast_phys(addr1), wv1);
         }
-        if (wr && !wram) {  // IO / MBC / SRAM / OAM DMA / flush before VRAM-OAM: out of line
+        if (wr & !wram) {  // rare: IO registers / MBC / SRAM / OAM DMA / IE
             St t = s;
             pk_write_slow(&A, c.g, c.lane, env, c.gid, &t, addr0, wv0, addr1, wv1, wr2 ? 1u : 0u);
             s = t;
-            ev |= PK_EV_WR_SLOW | sel(wvo, PK_EV_FLUSH, 0u);
+            ev |= PK_EV_WR_SLOW;
         }
         ev |= sel(wr, PK_EV_WR | sel(wr2, PK_EV_WR2, 0u) | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
                       | sel(addr0 >= 0xC000u && addr0 < 0xFE00u, PK_EV_WR_WRAM, sel(addr0 >= 0x8000u && addr0 < 0xA000u, PK_EV_WR_VRAM, 0u)), 0u);
