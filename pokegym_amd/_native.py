@@ -9,7 +9,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libpokegym_amd.so")
+# PK_LIB selects an alternative in-tree build (A/B kernel experiments); default: lib/libpokegym_amd.so
+LIB_PATH = os.environ.get("PK_LIB") or os.path.join(HERE, "lib", "libpokegym_amd.so")
 
 ABI_VERSION = 2
 PK_F_RENDER = 1

@@ -27,15 +27,17 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, out: str | None = None, extra: list | None = None) -> str:
+    """Compile the gfx950 library; `out`/`extra` build an alternative copy for A/B experiments."""
+    lib = out or LIB
+    if out is None and not force and not _stale():
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
     objs = []
     for src in SOURCES:
-        obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + ".o")
+        obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + (".alt.o" if out else ".o"))
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-               "-Wno-unused-function", "-Wno-bitwise-instead-of-logical", "-c", "-o", obj]
+               "-Wno-unused-function", "-Wno-bitwise-instead-of-logical", "-c", "-o", obj] + list(extra or [])
         if src.endswith(".cpp"):
             cmd += ["-x", "hip"]
         cmd.append(os.path.join(CSRC, src))
@@ -43,12 +45,12 @@ def build(force: bool = False, verbose: bool = False) -> str:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs, check=True)
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     for o in objs:
         os.remove(o)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":

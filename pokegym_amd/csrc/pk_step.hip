@@ -34,6 +34,11 @@
 #define CPU_QUEUED 4u
 #define CPU_CRASH 8u
 #define PK_NO_BANK 0xFFFFFFFFu
+// largest K1 workgroup: 256 envs per CU share one LDS copy of the ROM banks and microcode, so a
+// 16-lane wave shape needs 1024-thread workgroups (and <= 128 VGPRs)
+#ifndef PK_K1_MAX_THREADS
+#define PK_K1_MAX_THREADS 512
+#endif
 
 // debug hooks: the host-simulation build (tests/hostsim) records an instruction trace and
 // per-iteration event bits; the gfx950 build compiles them away.
@@ -274,7 +279,7 @@ __device__ __forceinline__ void pk_write_slow(const PkStepArgs* A, u8* g, u32 la
 
 // ---------------------------------------------------------------------------------------------
 // K1
-__global__ void __launch_bounds__(512) pk_step_kernel(PkStepArgs A) {
+__global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A) {
     for (u32 i = threadIdx.x; i < PK_UC_ENTRIES * PK_UE_WORDS; i += blockDim.x) lds_uc[i] = A.ucode[i];
     for (u32 i = threadIdx.x; i < 128u; i += blockDim.x) lds_slot[i] = A.bank_slot[i];
     for (u32 sl = 0; sl < A.nslots; sl++) {
@@ -666,7 +671,8 @@ hipError_t pk_launch_step(const PkStepArgs& a, hipStream_t s) {
     // of a CU (the ~115 KB of LDS staging allows one workgroup per CU)
     const u32 wl = a.wave_lanes;
     const u32 threads = a.npad * (PK_LANES / wl);
-    const u32 block = threads / PK_LANES <= a.simds ? 256u : 512u;
+    const u32 wide = 256u * PK_LANES / wl < PK_K1_MAX_THREADS ? 256u * PK_LANES / wl : PK_K1_MAX_THREADS;
+    const u32 block = threads / PK_LANES <= a.simds ? 256u : wide;
     const u32 grid = (threads + block - 1) / block;
     hipLaunchKernelGGL(pk_step_kernel, dim3(grid), dim3(block), 0, s, a);
     return hipGetLastError();

@@ -69,3 +69,16 @@ def test_load_snapshot_roundtrip():
     for i, st in enumerate(z["states"]):
         assert emu.snapshot(65 - i) == st.tobytes()
     emu.close()
+
+
+@pytest.mark.parametrize("lanes", ["64", "32", "16"])
+def test_game_rom_parity_wave_shapes(lanes, monkeypatch):
+    """The pkbench game (HALT/VBlank frame loop, HRAM OAM-DMA routine, MBC3 banking, SRAM) under
+    every K1 wave shape: 64, 32 or 16 envs per wave (PK_WAVE_LANES), with random actions."""
+    from pokegym_amd.testrom.game import game_rom
+    monkeypatch.setenv("PK_WAVE_LANES", lanes)
+    rom = game_rom()
+    n, steps = 96, 6
+    gpu, ref = _run_both(rom, None, n, steps, 7)
+    bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
+    assert not bad, bad[:4]
