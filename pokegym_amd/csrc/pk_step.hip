@@ -62,6 +62,13 @@ enum {
 __shared__ __attribute__((aligned(16))) u32 lds_uc[PK_UC_ENTRIES * PK_UE_WORDS];  // microcode
 __shared__ __attribute__((aligned(16))) u8 lds_rom[PK_LDS_SLOTS * 0x4000u + 16u]; // ROM banks (+ fetch overrun pad)
 __shared__ int8_t lds_slot[128];                                                  // bank -> slot
+// Fetch-only mirror of HRAM (0xFF80-0xFFFE) per env of the workgroup, byte (addr - 0xFF80) * 256 +
+// local env, + one dummy row: the OAM-DMA wait loop runs from HRAM, and fetching it from the HBM
+// image put a second dependent HBM round trip (fetch, then data) into ~30 % of wave iterations.
+// Data reads/writes stay on the image (authoritative); every HRAM write also updates the mirror
+// (lanes that do not write HRAM store to the dummy row, so the store needs no branch).
+#define PK_WG_ENVS 256u
+__shared__ u8 lds_hcode[128u * PK_WG_ENVS];
 
 // ---------------------------------------------------------------------------------------------
 // branch-free helpers: arguments are evaluated unconditionally, so ?: on them is a v_cndmask
@@ -92,10 +99,16 @@ struct Ctx {
     const PkStepArgs* A;
     u8* g;                // lane-interleaved RAM image of this wave's group
     u32 lane, env, gid;
+    u32 loc;              // env index within the workgroup (HRAM mirror column)
 };
 
 __device__ __forceinline__ u32 ld_img(const Ctx& c, u32 phys) { return c.g[phys * PK_LANES + c.lane]; }
 __device__ __forceinline__ void st_img(const Ctx& c, u32 phys, u32 v) { c.g[phys * PK_LANES + c.lane] = (u8)v; }
+// keep the HRAM fetch mirror in step with a RAM write at guest address a (row 127 = dummy)
+__device__ __forceinline__ void hcode_st(const Ctx& c, u32 a, u32 v) {
+    const u32 row = sel(a - 0xFF80u < 0x7Fu, a - 0xFF80u, 0x7Fu);
+    lds_hcode[row * PK_WG_ENVS + c.loc] = (u8)v;
+}
 
 // fast RAM: VRAM, WRAM, echo, OAM/unusable, HRAM — plain bytes of the image with no side effects
 __device__ __forceinline__ bool fast_ram(u32 a) {
@@ -249,28 +262,29 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
         s.npend = 0;
     }
     st_img(c, fast_phys(a), v);
+    hcode_st(c, a, v);
 }
 
 // ---- rare paths (operate on a copy of the lane state) ----
-__device__ __forceinline__ u32 pk_fetch_slow(const PkStepArgs* A, u8* g, u32 lane, const St* sp, u32 pc) {
+__device__ __forceinline__ u32 pk_fetch_slow(const PkStepArgs* A, u8* g, u32 lane, u32 loc, const St* sp, u32 pc) {
     Ctx c;
-    c.A = A; c.g = g; c.lane = lane; c.env = 0; c.gid = 0;
+    c.A = A; c.g = g; c.lane = lane; c.env = 0; c.gid = 0; c.loc = loc;
     const St s = *sp;
     return bus_read_any(c, s, pc) | (bus_read_any(c, s, (pc + 1u) & 0xFFFFu) << 8)
          | (bus_read_any(c, s, (pc + 2u) & 0xFFFFu) << 16);
 }
-__device__ __forceinline__ u32 pk_read_slow(const PkStepArgs* A, u8* g, u32 lane, const St* sp, u32 a0, u32 a1, u32 two) {
+__device__ __forceinline__ u32 pk_read_slow(const PkStepArgs* A, u8* g, u32 lane, u32 loc, const St* sp, u32 a0, u32 a1, u32 two) {
     Ctx c;
-    c.A = A; c.g = g; c.lane = lane; c.env = 0; c.gid = 0;
+    c.A = A; c.g = g; c.lane = lane; c.env = 0; c.gid = 0; c.loc = loc;
     const St s = *sp;
     const u32 m0 = bus_read_any(c, s, a0);
     const u32 m1 = two ? bus_read_any(c, s, a1) : 0u;
     return m0 | (m1 << 8);
 }
-__device__ __forceinline__ void pk_write_slow(const PkStepArgs* A, u8* g, u32 lane, u32 env, u32 gid, St* sp,
+__device__ __forceinline__ void pk_write_slow(const PkStepArgs* A, u8* g, u32 lane, u32 loc, u32 env, u32 gid, St* sp,
                                                   u32 a0, u32 v0, u32 a1, u32 v1, u32 two) {
     Ctx c;
-    c.A = A; c.g = g; c.lane = lane; c.env = env; c.gid = gid;
+    c.A = A; c.g = g; c.lane = lane; c.env = env; c.gid = gid; c.loc = loc;
     St s = *sp;
     bus_write_any(c, s, a0, v0);
     if (two) bus_write_any(c, s, a1, v1);
@@ -302,6 +316,8 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
     c.env = env;
     c.gid = __builtin_amdgcn_readfirstlane(env / PK_LANES);
     c.g = A.mem + (size_t)c.gid * PK_GROUP_STRIDE;
+    c.loc = (threadIdx.x >> 6) * A.wave_lanes + wl;  // < PK_WG_ENVS: <= 256 envs per workgroup
+    for (u32 i = 0; i < 0x7Fu; i++) lds_hcode[i * PK_WG_ENVS + c.loc] = (u8)ld_img(c, PK_P_HRAM + i);
 
     const u32 np = A.npad;
     u32* R = A.regs;
@@ -376,13 +392,17 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         // code outside the staged ROM (rare): RAM code such as the HRAM OAM-DMA wait loop reads the
         // image (three loads when pc..pc+2 stay in one 512-byte block of plain RAM), else the bus
         if (exec & !flds) {
-            if (fast_ram(pc) & fast_ram((pc + 2u) & 0xFFFFu) & (((pc ^ (pc + 2u)) & 0xFE00u) == 0u)) {
+            if (pc - 0xFF80u < 0x7Du) {  // pc..pc+2 inside HRAM: the LDS mirror
+                const u32 q = (pc - 0xFF80u) * PK_WG_ENVS + c.loc;
+                bytes = lds_hcode[q] | (lds_hcode[q + PK_WG_ENVS] << 8) | (lds_hcode[q + 2u * PK_WG_ENVS] << 16);
+                ev |= PK_EV_F_BUS | PK_EV_HRAM;
+            } else if (fast_ram(pc) & fast_ram((pc + 2u) & 0xFFFFu) & (((pc ^ (pc + 2u)) & 0xFE00u) == 0u)) {
                 const u32 p = fast_phys(pc);
                 bytes = ld_img(c, p) | (ld_img(c, p + 1u) << 8) | (ld_img(c, p + 2u) << 16);
                 ev |= PK_EV_F_BUS | sel(pc >= 0xFF80u, PK_EV_HRAM, 0u);
             } else {
                 const St t = s;
-                bytes = pk_fetch_slow(&A, c.g, c.lane, &t, pc);
+                bytes = pk_fetch_slow(&A, c.g, c.lane, c.loc, &t, pc);
                 ev |= PK_EV_F_ROM16;
             }
         }
@@ -431,7 +451,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
                 ev |= PK_EV_RD_IO;
             } else {
                 const St t = s;
-                const u32 m = pk_read_slow(&A, c.g, c.lane, &t, addr0, addr1, rd2 ? 1u : 0u);
+                const u32 m = pk_read_slow(&A, c.g, c.lane, c.loc, &t, addr0, addr1, rd2 ? 1u : 0u);
                 m0 = m & 0xFFu;
                 m1 = m >> 8;
                 ev |= PK_EV_RD_ROMG;
@@ -519,11 +539,15 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
                 ev |= PK_EV_FLUSH;
             }
             st_img(c, fast_phys(addr0), wv0);
-            if (wr2) st_img(c, fast_phys(addr1), wv1);
+            hcode_st(c, addr0, wv0);
+            if (wr2) {
+                st_img(c, fast_phys(addr1), wv1);
+                hcode_st(c, addr1, wv1);
+            }
         }
         if (wr & !wram) {  // rare: IO registers / MBC / SRAM / OAM DMA / IE
             St t = s;
-            pk_write_slow(&A, c.g, c.lane, env, c.gid, &t, addr0, wv0, addr1, wv1, wr2 ? 1u : 0u);
+            pk_write_slow(&A, c.g, c.lane, c.loc, env, c.gid, &t, addr0, wv0, addr1, wv1, wr2 ? 1u : 0u);
             s = t;
             ev |= PK_EV_WR_SLOW;
         }
