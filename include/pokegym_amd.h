@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PK_ABI_VERSION 2
+#define PK_ABI_VERSION 3
 #define PK_STATE_V9_BYTES 142610u
 #define PK_SCREEN_ROWS 144u
 #define PK_SCREEN_COLS 160u
@@ -56,6 +56,10 @@ extern "C" {
 #define PK_ERR_HEATMAP_INDEX 5  /* IndexError, counts_map outside 444x436 (:676) */
 #define PK_ERR_BUS_INDEX 6      /* IndexError, memory read past 0xFFFF (box scan, :574-578) */
 #define PK_ERR_CAPACITY 7       /* device table full (no reference equivalent) */
+
+/* info telemetry record: the numeric scalars of info["stats"] (57) and info["reward"] (21),
+ * environment.py:1621-1704, field order pokegym_amd/info.py FIELDS */
+#define PK_INFO_NFIELDS 78
 
 typedef struct pk_config {
     uint32_t n_envs;             /* envs on this GPU */
@@ -101,6 +105,13 @@ uint8_t* pk_screen_ptr(pk_handle* h);
 uint8_t* pk_obs_ptr(pk_handle* h);
 /* device pointer to u32[n] PK_ERR_* codes (PK_F_REWARD), sticky until the env's next reset */
 const uint32_t* pk_error_ptr(pk_handle* h);
+/* device pointers to the info telemetry of the last pk_step (PK_F_REWARD).  info_flag u8[n] = 1
+ * where the reference's step built its info dict (done or time % 10000 == 0, environment.py:1621);
+ * for those envs info f64[PK_INFO_NFIELDS][npad] (field-major, env stride = npad, the padded
+ * env count: pk_info_stride) holds the record.  Replaces the info dict of Environment.step. */
+const double* pk_info_ptr(pk_handle* h);
+const uint8_t* pk_info_flag_ptr(pk_handle* h);
+uint32_t pk_info_stride(const pk_handle* h);
 
 /* Stream-ordered bulk RAM access for all envs: dense_dev[e * len + i] <-> guest address
  * addr + i of env e.  RAM regions only (0xC000-0xFDFF incl. echo, 0xFF80-0xFFFE). */

@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # PK_LIB selects an alternative in-tree build (A/B kernel experiments); default: lib/libpokegym_amd.so
 LIB_PATH = os.environ.get("PK_LIB") or os.path.join(HERE, "lib", "libpokegym_amd.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 PK_F_RENDER = 1
 PK_F_REWARD = 2
 PK_F_RELOAD_ON_RESET = 4
@@ -27,7 +27,7 @@ ROWS, COLS = 144, 160
 EXPORTS = ("pk_create", "pk_destroy", "pk_last_error", "pk_abi_version", "pk_reset", "pk_step",
            "pk_screen_ptr", "pk_num_envs", "pk_peek", "pk_poke", "pk_snapshot", "pk_load_env",
            "pk_last_instr_count", "pk_profile_enable", "pk_profile_read", "pk_obs_ptr", "pk_error_ptr",
-           "pk_get_ram", "pk_set_ram")
+           "pk_get_ram", "pk_set_ram", "pk_info_ptr", "pk_info_flag_ptr", "pk_info_stride")
 
 
 class PkConfig(ctypes.Structure):
@@ -94,6 +94,12 @@ def bind_v2(L):
     L.pk_obs_ptr.restype = vp
     L.pk_error_ptr.argtypes = [vp]
     L.pk_error_ptr.restype = vp
+    L.pk_info_ptr.argtypes = [vp]
+    L.pk_info_ptr.restype = vp
+    L.pk_info_flag_ptr.argtypes = [vp]
+    L.pk_info_flag_ptr.restype = vp
+    L.pk_info_stride.argtypes = [vp]
+    L.pk_info_stride.restype = ctypes.c_uint32
     L.pk_get_ram.argtypes = [vp, ctypes.c_uint16, ctypes.c_uint32, vp, vp]
     L.pk_set_ram.argtypes = [vp, ctypes.c_uint16, ctypes.c_uint32, vp, vp]
     L.pk_reset.argtypes = [vp, vp, vp]

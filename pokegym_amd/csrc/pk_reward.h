@@ -62,6 +62,14 @@ enum { RSD_LAST_REWARD = 0, RSD_TOTAL_HEALING, RSD_LAST_HP, RSD_NFIELDS };
 #define PKE_BUS_INDEX 6u
 #define PKE_CAPACITY 7u       // device table full (no reference equivalent)
 
+// info telemetry record (environment.py:1621-1704; field order = pokegym_amd/info.py FIELDS)
+#define PK_INFO_NSTATS 57u
+#define PK_INFO_NREWARD 21u
+#ifndef PK_INFO_NFIELDS
+#define PK_INFO_NFIELDS 78u   // == include/pokegym_amd.h
+#endif
+static_assert(PK_INFO_NFIELDS == PK_INFO_NSTATS + PK_INFO_NREWARD, "info record layout");
+
 #define PK_CUTC_CAP 64u
 #define PK_MASK_WORDS 2048u   // 256 rows x 8 words
 #define PK_OBS_H 72u
@@ -84,6 +92,8 @@ struct PkRewardArgs {
     double* rew;              // [n] or null
     uint8_t* term;            // [n] or null
     uint8_t* trunc;           // [n] or null
+    double* info;             // [PK_INFO_NFIELDS][npad] info record, written where info_flag = 1
+    uint8_t* info_flag;       // [n] 1 = this step built the reference's info dict (done or time % 10000 == 0)
     double reward_scale;
     uint32_t n, npad;
     uint32_t cap_log2;        // seen table capacity = 1 << cap_log2

@@ -241,6 +241,7 @@ __global__ void __launch_bounds__(256) pk_reward_kernel(PkRewardArgs A) {
     const bool done = time >= A.max_steps;          // :1613
     if (A.term) A.term[e] = done ? 1 : 0;
     if (A.trunc) A.trunc[e] = done ? 1 : 0;
+    if (A.info_flag) A.info_flag[e] = 0;
     if (rs[RS_ERR * np + e]) {                      // the reference env raised: frozen
         if (A.rew) A.rew[e] = 0.0;
         return;
@@ -535,6 +536,52 @@ __global__ void __launch_bounds__(256) pk_reward_kernel(PkRewardArgs A) {
         rs[RS_MASK_MAP * np + e] = map;
     }
     mask_set(mk, r, c);
+
+    // info telemetry (:1621-1704): built on done or every 10000th step; rare, so its extra peeks
+    // stay off the common path.  Every numeric scalar of info["stats"] / info["reward"].
+    if (A.info && !M.err && (done || time % 10000u == 0u)) {
+        u32 lv[6], hi = 0;
+        for (u32 k = 0; k < 6u; k++) { lv[k] = rd(M, k_party_level[k]); hi = max(hi, lv[k]); }
+        {   // highest_pokemon_level = max(nonzero levels); the reference raises ValueError (max([]),
+            // :1672) for an empty party — telemetry does not kill the env here, the record holds 0
+            const u32 nb = badges_reward / 10u;
+            const u32 d7b1 = rd(M, 0xD7B1);
+            auto bcd = [](u32 v) { return 10u * ((v >> 4) & 0xFu) + (v & 0xFu); };
+            const u32 money = 10000u * bcd(rd(M, 0xD347)) + 100u * bcd(rd(M, 0xD348)) + bcd(rd(M, 0xD349));
+            double* o = A.info + e;
+            u32 f = 0;
+            auto put = [&](double v) { o[(size_t)(f++) * np] = v; };
+            put((double)time); put((double)c); put((double)r); put((double)map); put((double)party_size);
+            for (u32 k = 0; k < 6u; k++) put((double)lv[k]);
+            put((double)lsum);                      // levels_sum (raw levels)
+            put((double)deaths); put((double)deaths);  // deaths, deaths_per_episode (both reset, :1269, :1297)
+            put((double)nb); put(0.0);              // badges, self.badge_count (never updated)
+            for (u32 k = 1; k <= 6u; k++) put(nb >= k ? 1.0 : 0.0);
+            put(0.0);                               // events = len(past_events_string) = 0 after reset (:1301)
+            put((double)rs[RS_MAX_OPP * np + e]);
+            put((double)rbit(M, 0xD7F1, 0));
+            for (u32 b = 3; b <= 7u; b++) put((double)rbit(M, 0xD7F2, b));
+            put((double)rbit(M, 0xD803, 0)); put((double)rbit(M, 0xD803, 1));
+            put((double)party_size); put((double)hi); put((double)lsum); put((double)events); put((double)money);
+            put(0.0);                               // seen_npcs_count
+            put((double)seen_cnt); put((double)caught_cnt); put((double)moves_cnt);
+            put(0.0);                               // hidden_obj_count
+            put((double)(bill_reward / 5u)); put((double)hm_count); put((flags & RSF_CUT) ? 1.0 : 0.0);
+            put((double)bill_capt / 5.0); put(cut_coords * 1.0); put((double)ntiles * 1.0);
+            put(bag_menu); put(stats_menu); put(pokemon_menu); put(start_menu);
+            put((double)used_cut2); put(0.0);       // used_cut, state_loaded_instead_of_resetting_in_game
+            put((double)(d7b1 & 1u)); put((double)(3u * ((d7b1 >> 6) & 1u))); put((double)(3u * ((d7b1 >> 7) & 1u)));
+            // info["reward"]
+            put(reward); put((double)max_events); put(level_reward);
+            put(0.006 * (double)rs[RS_MAX_OPP * np + e]); put(0.0);
+            put((double)badges_reward); put((double)bill_reward); put((double)hm_reward);
+            put(total_healing); put(exploration);
+            put(scale * (double)seen_cnt); put(scale * (double)caught_cnt); put(scale * (double)moves_cnt);
+            put((double)cut_rew); put(tree); put((double)dojo);
+            for (u32 t = 0; t < 5u; t++) put(((flags >> (8u + t)) & 1u) ? 20.0 : 0.0);
+            if (A.info_flag) A.info_flag[e] = 1;
+        }
+    }
 
     rs[RS_FLAGS * np + e] = flags;
     rs[RS_SEEN_N * np + e] = seen_n;

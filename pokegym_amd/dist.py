@@ -66,3 +66,34 @@ class EpisodeStats:
 
     def reset_summary(self):
         self.summary.zero_()
+
+
+class InfoStats:
+    """Device-side sum of the info telemetry records (pokegym_amd/info.py) of every env that emitted
+    one, plus their count; all-reduced and averaged per logging interval, like PufferLib's mean over
+    the info dicts its envs returned."""
+
+    def __init__(self, device):
+        from .info import NFIELDS
+        self.device = torch.device(device)
+        self.sum = torch.zeros(NFIELDS + 1, dtype=torch.float64, device=self.device)   # last = count
+
+    def update(self, info: torch.Tensor, flag: torch.Tensor):
+        """info: f64 (NFIELDS, n) view, flag: (n,) 0/1 — one GEMV, no host sync."""
+        f = flag.to(torch.float64)
+        self.sum[:-1] += torch.mv(info, f)
+        self.sum[-1] += f.sum()
+
+    def allreduce(self, group=None, reset: bool = True) -> dict:
+        from .info import REWARD_FIELDS, STATS_FIELDS
+        out = self.sum.clone()
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
+        if reset:
+            self.sum.zero_()
+        vals = out.tolist()
+        n = vals[-1]
+        mean = [v / n if n else float("nan") for v in vals[:-1]]
+        ns = len(STATS_FIELDS)
+        return {"info_records": n, "stats": dict(zip(STATS_FIELDS, mean[:ns])),
+                "reward": dict(zip(REWARD_FIELDS, mean[ns:]))}

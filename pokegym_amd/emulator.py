@@ -15,6 +15,7 @@ import numpy as np
 import torch
 
 from . import _native
+from .info import NFIELDS, info_dict
 from ._native import (COLS, ERR_EXCEPTIONS, OBS_SHAPE, PK_F_RELOAD_ON_RESET, PK_F_RENDER, PK_F_REWARD, ROWS,
                       STATE_V9_BYTES, check)
 
@@ -69,11 +70,19 @@ class BatchedEmulator:
         self.screen = torch.as_tensor(_CudaArray(ptr, (self.n, ROWS, COLS), "|u1"), device=self.device)
         self.obs = None
         self.errors = None
+        self.info = None        # f64 (PK_INFO_NFIELDS, n) view, field-major (pokegym_amd/info.py FIELDS)
+        self.info_flag = None   # u8 (n,): 1 where the last step built the reference's info dict
         if reward:
             self.obs = torch.as_tensor(_CudaArray(self._L.pk_obs_ptr(self._h), (self.n,) + OBS_SHAPE, "|u1"),
                                        device=self.device)
             self.errors = torch.as_tensor(_CudaArray(self._L.pk_error_ptr(self._h), (self.n,), "<i4"),
                                           device=self.device)
+            stride = int(self._L.pk_info_stride(self._h))
+            full = torch.as_tensor(_CudaArray(self._L.pk_info_ptr(self._h), (NFIELDS, stride), "<f8"),
+                                   device=self.device)
+            self.info = full[:, :self.n]
+            self.info_flag = torch.as_tensor(_CudaArray(self._L.pk_info_flag_ptr(self._h), (self.n,), "|u1"),
+                                             device=self.device)
         self.rewards = torch.zeros(self.n, dtype=torch.float64, device=self.device)
         self.terminals = torch.zeros(self.n, dtype=torch.uint8, device=self.device)
         self.truncations = torch.zeros(self.n, dtype=torch.uint8, device=self.device)
@@ -114,6 +123,19 @@ class BatchedEmulator:
             e = int(bad[0]) + (0 if env is None else env)
             code = int(self.errors[e])
             raise ERR_EXCEPTIONS.get(code, RuntimeError)(f"env {e}: reference reward stack raises here (PK_ERR {code})")
+
+    def info_dicts(self, envs=None) -> dict:
+        """{env: info dict} for the envs whose last step built one (host sync; environment.py:1621-1704)."""
+        if self.info_flag is None:
+            return {}
+        flag = self.info_flag if envs is None else self.info_flag[envs]
+        ids = torch.nonzero(flag).flatten()
+        if envs is not None:
+            ids = torch.as_tensor(envs, device=self.device).reshape(-1)[ids]
+        if not ids.numel():
+            return {}
+        rec = self.info[:, ids].t().cpu().numpy()
+        return {int(e): info_dict(r) for e, r in zip(ids.tolist(), rec)}
 
     # -- bulk RAM views (stream-ordered) ------------------------------------------------
     def get_ram(self, addr: int, length: int, out: torch.Tensor | None = None) -> torch.Tensor:
@@ -168,6 +190,7 @@ class BatchedEmulator:
             self.screen = None
             self.obs = None
             self.errors = None
+            self.info = self.info_flag = None
             self._L.pk_destroy(self._h)
             self._h = None
 

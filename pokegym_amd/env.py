@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from . import spaces
-from .dist import EpisodeStats, env_rank, shard_range
+from .dist import EpisodeStats, InfoStats, env_rank, shard_range
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_STATE = os.path.join(HERE, "states", "Bulbasaur.state")  # environment.py:119-120
@@ -60,12 +60,14 @@ class Environment:
         return obs[0].cpu().numpy(), {}
 
     def step(self, action, fast_video=True):
-        """environment.py:1336-1812; info is {} (the reference fills it only at done / every 10k steps)."""
+        """environment.py:1336-1812; info is {} except at done / every 10000th step (:1621), where it
+        holds the numeric scalars of the reference's "stats" and "reward" dicts (pokegym_amd/info.py)."""
         a = torch.tensor([int(action)], dtype=torch.uint8, device=self.emu.device)
         obs, rew, term, trunc = self.emu.step(a)
         self.emu.raise_if_failed(0)
         done = bool(term[0].item())
-        return obs[0].cpu().numpy(), float(rew[0].item()), done, done, {}
+        info = self.emu.info_dicts([0]).get(0, {})
+        return obs[0].cpu().numpy(), float(rew[0].item()), done, done, info
 
     def render(self):
         return self.emu.obs[0].cpu().numpy()
@@ -95,6 +97,7 @@ class VecEnv:
         self.env_ids = torch.arange(env_offset, env_offset + num_envs, device=self.device)
         self.masks = torch.ones(num_envs, dtype=torch.bool, device=self.device)
         self.stats = EpisodeStats(num_envs, self.device)
+        self.info_stats = InfoStats(self.device) if getattr(emulator, "info", None) is not None else None
         self.log_interval = log_interval
         self.t = 0
         self._pending = None
@@ -113,6 +116,8 @@ class VecEnv:
         terminals = term.to(torch.bool)
         truncations = trunc.to(torch.bool)
         self.stats.update(rewards, term)
+        if self.info_stats is not None:
+            self.info_stats.update(self.emu.info, self.emu.info_flag)
         self.emu.reset(term)  # auto-reset finished envs (no host sync)
         self.t += 1
         infos = []
@@ -120,6 +125,8 @@ class VecEnv:
             if hasattr(self.emu, "raise_if_failed"):
                 self.emu.raise_if_failed()
             infos = [self.stats.allreduce()]
+            if self.info_stats is not None:
+                infos[0].update(self.info_stats.allreduce())
         return obs, rewards, terminals, truncations, infos
 
     # PufferLib async API

@@ -6,6 +6,7 @@ import ctypes
 import numpy as np
 
 from pokegym_amd._native import PK_F_REWARD, PkConfig, bind_v2
+from pokegym_amd.info import NFIELDS as PK_INFO_NFIELDS
 
 import sim
 
@@ -73,3 +74,12 @@ class HostsimRewardBackend:
     def set_screen(self, h, screen):
         p = self.L.pk_screen_ptr(h)
         ctypes.memmove(p, np.ascontiguousarray(screen, np.uint8).ctypes.data, 144 * 160)
+
+    def info(self, h):
+        """The step's info record (pokegym_amd/info.py FIELDS) or None (pk_info_ptr / pk_info_flag_ptr)."""
+        f = ctypes.cast(self.L.pk_info_flag_ptr(h), ctypes.POINTER(ctypes.c_uint8))[0]
+        if not f:
+            return None
+        stride = int(self.L.pk_info_stride(h))
+        p = ctypes.cast(self.L.pk_info_ptr(h), ctypes.POINTER(ctypes.c_double))
+        return [p[i * stride] for i in range(PK_INFO_NFIELDS)]

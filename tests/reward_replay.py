@@ -119,3 +119,59 @@ def run_replay(backend, base_state: bytes, g, seqs):
         finally:
             backend.destroy(h)
     return n_checked
+
+
+# ---------------------------------------------------------------------------------------------
+# info telemetry (tests/golden/info_stats.npz, tools/make_golden_info.py): short episodes, the
+# record of every step whose info dict was non-empty (done or time % 10000 == 0)
+def info_sequences():
+    """-> (golden dict, list of (seq_index, max_steps, W, H, S, A))."""
+    d = np.load(os.path.join(HERE, "golden", "info_stats.npz"))
+    g = {k: d[k] for k in d.files}
+    bw, bh = replay_gen.load_bank()
+    dims = dict(T.MAP_DIMS)
+    out = []
+    for si, (seed, steps, max_steps, allow_err, scen) in enumerate(g["seqs"].tolist()):
+        W, H, S, A = replay_gen.make_sequence(bw, bh, seed, steps, dims, bool(allow_err), scen, T.MAP_COORD)
+        out.append((si, int(max_steps), W, H, S, A))
+    return g, out
+
+
+def check_info(g, got):
+    """got: {(seq, t): record} -> asserts it equals the golden records (same steps, same values)."""
+    exp = {(int(s), int(t)): v for s, t, v in zip(g["seq"], g["t"], g["values"])}
+    assert sorted(got) == sorted(exp), (sorted(set(got) ^ set(exp))[:8])
+    fields = [str(f) for f in g["fields"]]
+    for k, v in exp.items():
+        bad = [(fields[i], float(got[k][i]), float(v[i])) for i in range(len(v)) if float(got[k][i]) != float(v[i])]
+        assert not bad, (k, bad[:6])
+    return len(exp)
+
+
+def run_info_replay(backend, base_state: bytes):
+    """The info records `backend` emits over the info golden sequences (1-env handle per sequence;
+    a sequence ends at its first error, as the reference raised there)."""
+    g, seqs = info_sequences()
+    got = {}
+    for si, max_steps, W, H, S, A in seqs:
+        h = backend.create(template_state(base_state, W[0], H[0], S[0]), max_steps)
+        try:
+            backend.reset(h)
+            if backend.error(h):
+                continue
+            for t in range(1, len(A) + 1):
+                backend.set_ram(h, W[t], H[t])
+                backend.set_screen(h, S[t])
+                _, d = backend.step(h, int(A[t - 1]))
+                if backend.error(h):
+                    break
+                rec = backend.info(h)
+                if rec is not None:
+                    got[(si, t)] = np.asarray(rec, np.float64)
+                if d:
+                    backend.reset(h)
+                    if backend.error(h):
+                        break
+        finally:
+            backend.destroy(h)
+    return g, got

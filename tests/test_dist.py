@@ -12,7 +12,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from pokegym_amd.dist import STAT_FIELDS, EpisodeStats, shard_range
+from pokegym_amd.dist import STAT_FIELDS, EpisodeStats, InfoStats, shard_range
+from pokegym_amd.info import NFIELDS
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -72,6 +73,33 @@ def test_stats_allreduce_gloo_world2(tmp_path):
     got = [eval(open(tmp_path / f"stats{r}.txt").read()) for r in range(2)]
     # episodes: 2 per rank; returns: 2*1 + 2*2; lengths 4; reward sums 4*1 + 4*2; steps 8
     assert got[0] == got[1] == [6.0, 4.0, 4.0, 12.0, 8.0]
+
+
+def test_info_stats_mean_of_emitted_records():
+    st = InfoStats("cpu")
+    info = torch.arange(NFIELDS * 3, dtype=torch.float64).reshape(NFIELDS, 3)
+    st.update(info, torch.tensor([1, 0, 1], dtype=torch.uint8))
+    st.update(info * 0, torch.tensor([0, 0, 0], dtype=torch.uint8))
+    s = st.allreduce()
+    assert s["info_records"] == 2
+    assert s["stats"]["step"] == (0 + 2) / 2 and s["reward"]["has_bicycle_in_bag_reward"] == (NFIELDS - 1) * 3 + 1
+    assert st.sum.abs().sum() == 0   # reset after the read
+
+
+def _info_fn(rank, world, out_dir):
+    st = InfoStats("cpu")
+    info = torch.full((NFIELDS, 4), float(rank + 1), dtype=torch.float64)
+    st.update(info, torch.tensor([1, 1, 0, rank], dtype=torch.uint8))
+    s = st.allreduce()
+    with open(os.path.join(out_dir, f"info{rank}.txt"), "w") as f:
+        f.write(repr([s["info_records"], s["stats"]["money"], s["reward"]["delta"]]))
+
+
+def test_info_stats_allreduce_gloo_world2(tmp_path):
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), _info_fn), nprocs=2, join=True)
+    got = [eval(open(tmp_path / f"info{r}.txt").read()) for r in range(2)]
+    # rank 0: 2 records of 1.0, rank 1: 3 records of 2.0 -> mean 8/5
+    assert got[0] == got[1] == [5.0, 1.6, 1.6]
 
 
 N_ENVS, STEPS = 6, 2

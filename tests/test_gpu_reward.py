@@ -51,6 +51,11 @@ class GpuRewardBackend:
         import torch
         h.screen[0].copy_(torch.from_numpy(np.ascontiguousarray(s)))
 
+    def info(self, h):
+        if not int(h.info_flag[0].item()):
+            return None
+        return h.info[:, 0].cpu().numpy()
+
 
 @pytest.mark.gpu
 def test_gpu_reward_kernels_match_reference_replay():
@@ -58,6 +63,43 @@ def test_gpu_reward_kernels_match_reference_replay():
     g, seqs = sequences()
     base = open(os.path.join(REPO, "pokegym_amd", "states", "Bulbasaur.state"), "rb").read()
     assert run_replay(GpuRewardBackend(game_rom()), base, g, seqs) > 1500
+
+
+@pytest.mark.gpu
+def test_gpu_info_record_matches_reference():
+    """K4's info telemetry record (pk_info_ptr) against the reference's info dicts."""
+    from reward_replay import check_info, run_info_replay
+    from pokegym_amd.testrom.game import game_rom
+    base = open(os.path.join(REPO, "pokegym_amd", "states", "Bulbasaur.state"), "rb").read()
+    g, got = run_info_replay(GpuRewardBackend(game_rom()), base)
+    assert check_info(g, got) > 100
+
+
+@pytest.mark.gpu
+def test_gpu_environment_info_dict_and_vecenv_info_stats():
+    """Environment.step returns the reference-shaped info dict at done; VecEnv all-reduces the
+    device-side info sums at its logging interval."""
+    import torch
+    from pokegym_amd.env import Environment, VecEnv
+    from pokegym_amd.info import STATS_FIELDS
+    from pokegym_amd.testrom.game import game_rom
+    rom = game_rom()
+    env = Environment(rom_path=rom, max_episode_steps=3)
+    env.reset()
+    infos = [env.step(0)[4] for _ in range(3)]
+    assert infos[0] == {} and infos[1] == {}
+    st = infos[2]["stats"]
+    assert st["step"] == 3 and len(st["levels"]) == 6 and set(infos[2]["reward"]) >= {"delta", "exploration"}
+    assert set(STATS_FIELDS) - set(st) == {f"levels_{i}" for i in range(6)}
+    env.close()
+    v = VecEnv(64, rom=rom, max_episode_steps=2, log_interval=4)
+    v.reset()
+    out = None
+    for _ in range(4):
+        out = v.step(torch.zeros(64, dtype=torch.uint8))
+    info = out[4][0]
+    assert info["info_records"] == 128 and info["stats"]["step"] == 2.0
+    v.close()
 
 
 class _GBBus:

@@ -1,0 +1,47 @@
+"""The info telemetry restatement (oracle/reward.py step -> st.info) against the reference's
+own info dicts (tests/golden/info_stats.npz, tools/make_golden_info.py: every numeric scalar of
+info["stats"] / info["reward"], environment.py:1621-1704, at each done step of short episodes)."""
+import numpy as np
+
+from oracle import reward as R
+from pokegym_amd import info as I
+from reward_replay import check_info, info_sequences, install
+
+
+def test_info_fields_match_golden_layout():
+    g, _ = info_sequences()
+    assert [str(f) for f in g["fields"]] == list(I.STATS_FIELDS) + list(I.REWARD_FIELDS)
+    assert I.NFIELDS == len(g["fields"]) and len(g["values"]) > 100
+
+
+def test_oracle_info_matches_reference():
+    g, seqs = info_sequences()
+    got = {}
+    for si, max_steps, W, H, S, A in seqs:
+        mem = np.zeros(0x10000, np.uint8)
+        bus = R.Bus(mem)
+        st = R.EnvState()
+        install(mem, W[0], H[0])
+        R.reset(st, bus, S[0], reload=lambda: install(mem, W[0], H[0]), max_episode_steps=max_steps)
+        if st.err:
+            continue
+        for t in range(1, len(A) + 1):
+            install(mem, W[t], H[t])
+            _, _, done = R.step(st, bus, int(A[t - 1]), S[t])
+            if st.err:
+                break
+            if st.info is not None:
+                got[(si, t)] = st.info
+            if done:
+                R.reset(st, bus, S[t], max_episode_steps=max_steps)
+                if st.err:
+                    break
+    assert check_info(g, got) > 100
+
+
+def test_info_dict_shape():
+    rec = np.arange(I.NFIELDS, dtype=np.float64)
+    d = I.info_dict(rec)
+    assert d["stats"]["levels"] == [5, 6, 7, 8, 9, 10] and d["stats"]["step"] == 0
+    assert d["reward"]["has_bicycle_in_bag_reward"] == float(I.NFIELDS - 1)
+    assert isinstance(d["stats"]["badges"], float) and isinstance(d["stats"]["money"], int)
