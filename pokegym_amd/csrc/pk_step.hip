@@ -73,6 +73,8 @@ __shared__ u8 lds_hcode[128u * PK_WG_ENVS];
 // ---------------------------------------------------------------------------------------------
 // branch-free helpers: arguments are evaluated unconditionally, so ?: on them is a v_cndmask
 __device__ __forceinline__ u32 sel(bool c, u32 a, u32 b) { return c ? a : b; }
+// TIMA input clock divider as a shift: TAC & 3 = 0/1/2/3 -> 1024/16/64/256 cycles
+__device__ __forceinline__ u32 timer_shift(u32 tac) { return (0x0806040Au >> (8u * (tac & 3u))) & 0xFFu; }
 __device__ __forceinline__ u32 bit(u32 w, int pos) { return (w >> pos) & 1u; }
 __device__ __forceinline__ int sfield(u32 w, int pos, int bits) { return ((int)(w << (32 - pos - bits))) >> (32 - bits); }
 __device__ __forceinline__ u32 perm(u32 hi, u32 lo, u32 s) { return __builtin_amdgcn_perm(hi, lo, s); }
@@ -364,6 +366,11 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
     const u32* romw = reinterpret_cast<const u32*>(lds_rom);
 
     u32 budget = 0;  // frame watchdog (oracle/gbcore.c PK_FRAME_BUDGET)
+    // software pipeline: the next instruction's bytes and microcode entry, loaded from LDS at the
+    // end of the previous iteration (after its writes, so bank switches and HRAM code stores are
+    // seen) while the timer/LCD work runs; pf = 0 -> fetch and decode at the top instead
+    u32 pf = 0, pbytes = 0;
+    uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0, p2 = p0;
     while (frame < A.frames) {
         u32 ev = 0;
         // ---------------- front-end: cpu.tick / check_interrupts ----------------
@@ -373,6 +380,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         bool exec = true, doint = false, dispatch = false;
         u32 pc = s.pc, intflag = 0;
         if ((cpu0 & (CPU_CRASH | CPU_HALT | CPU_QUEUED)) | pend) {
+            pf = 0;
             const bool crashed = (cpu0 & CPU_CRASH) != 0u;
             const bool halted = (cpu0 & CPU_HALT) != 0u;
             const bool queued = (cpu0 & CPU_QUEUED) != 0u;
@@ -385,37 +393,44 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             s.cpu = sel(doint, (cpu0 | CPU_QUEUED) & ~CPU_HALT, sel(wake, cpu0 & ~CPU_HALT, cpu0)) ^ sel(dispatch, intflag << 16, 0u);
         }
 
-        // ---------------- fetch: LDS-staged ROM for every lane; other code out of line ----------------
-        const bool flds = rom_staged(s, pc) && (pc & 0x3FFFu) < 0x3FFEu;
-        const u32 la = sel(flds, rom_lds_index(s, pc), 0u);
-        u32 bytes = __builtin_amdgcn_alignbyte(romw[(la >> 2) + 1u], romw[la >> 2], la & 3u);
-        // code outside the staged ROM (rare): RAM code such as the HRAM OAM-DMA wait loop reads the
-        // image (three loads when pc..pc+2 stay in one 512-byte block of plain RAM), else the bus
-        if (exec & !flds) {
-            if (pc - 0xFF80u < 0x7Du) {  // pc..pc+2 inside HRAM: the LDS mirror
-                const u32 q = (pc - 0xFF80u) * PK_WG_ENVS + c.loc;
-                bytes = lds_hcode[q] | (lds_hcode[q + PK_WG_ENVS] << 8) | (lds_hcode[q + 2u * PK_WG_ENVS] << 16);
-                ev |= PK_EV_F_BUS | PK_EV_HRAM;
-            } else if (fast_ram(pc) & fast_ram((pc + 2u) & 0xFFFFu) & (((pc ^ (pc + 2u)) & 0xFE00u) == 0u)) {
-                const u32 p = fast_phys(pc);
-                bytes = ld_img(c, p) | (ld_img(c, p + 1u) << 8) | (ld_img(c, p + 2u) << 16);
-                ev |= PK_EV_F_BUS | sel(pc >= 0xFF80u, PK_EV_HRAM, 0u);
-            } else {
-                const St t = s;
-                bytes = pk_fetch_slow(&A, c.g, c.lane, c.loc, &t, pc);
-                ev |= PK_EV_F_ROM16;
+        // ---------------- fetch + microcode entry (prefetched, or here when pf = 0) ----------------
+        u32 bytes = pbytes;
+        uint4 e0 = p0, e1 = p1, e2 = p2;
+        if (!pf) {
+            const bool flds = rom_staged(s, pc) && (pc & 0x3FFFu) < 0x3FFEu;
+            const u32 la = sel(flds, rom_lds_index(s, pc), 0u);
+            bytes = __builtin_amdgcn_alignbyte(romw[(la >> 2) + 1u], romw[la >> 2], la & 3u);
+            // code outside the staged ROM (rare): RAM code such as the HRAM OAM-DMA wait loop reads the
+            // image (three loads when pc..pc+2 stay in one 512-byte block of plain RAM), else the bus
+            if (exec & !flds) {
+                if (pc - 0xFF80u < 0x7Du) {  // pc..pc+2 inside HRAM: the LDS mirror
+                    const u32 q = (pc - 0xFF80u) * PK_WG_ENVS + c.loc;
+                    bytes = lds_hcode[q] | (lds_hcode[q + PK_WG_ENVS] << 8) | (lds_hcode[q + 2u * PK_WG_ENVS] << 16);
+                    ev |= PK_EV_F_BUS | PK_EV_HRAM;
+                } else if (fast_ram(pc) & fast_ram((pc + 2u) & 0xFFFFu) & (((pc ^ (pc + 2u)) & 0xFE00u) == 0u)) {
+                    const u32 p = fast_phys(pc);
+                    bytes = ld_img(c, p) | (ld_img(c, p + 1u) << 8) | (ld_img(c, p + 2u) << 16);
+                    ev |= PK_EV_F_BUS | sel(pc >= 0xFF80u, PK_EV_HRAM, 0u);
+                } else {
+                    const St t = s;
+                    bytes = pk_fetch_slow(&A, c.g, c.lane, c.loc, &t, pc);
+                    ev |= PK_EV_F_ROM16;
+                }
             }
+            const u32 op = bytes & 0xFFu;
+            // INT pseudo-op: the vector rides in imm16
+            bytes = sel(exec, bytes, (0x40u + 8u * (u32)__builtin_ctz(intflag | 0x20u)) << 8);
+            const u32 di = sel(exec, sel(op == 0xCBu, 256u + ((bytes >> 8) & 0xFFu), op),
+                               sel(dispatch, PK_UC_INT, sel(doint, PK_UC_NOP0, PK_UC_IDLE)));
+            ev |= sel(exec, sel(flds, PK_EV_F_LDS, 0u), 0u);
+            e0 = ucv[di * 3u];
+            e1 = ucv[di * 3u + 1u];
+            e2 = ucv[di * 3u + 2u];
         }
-        const u32 op = bytes & 0xFFu;
-        // INT pseudo-op: the vector rides in imm16
-        bytes = sel(exec, bytes, (0x40u + 8u * (u32)__builtin_ctz(intflag | 0x20u)) << 8);
-        const u32 di = sel(exec, sel(op == 0xCBu, 256u + ((bytes >> 8) & 0xFFu), op),
-                           sel(dispatch, PK_UC_INT, sel(doint, PK_UC_NOP0, PK_UC_IDLE)));
         icount += sel(exec, 1u, 0u);
-        ev |= sel(exec, PK_EV_EXEC | sel(flds, PK_EV_F_LDS, 0u) | sel(op == 0xCBu, PK_EV_CB, 0u), 0u)
+        ev |= sel(exec, PK_EV_EXEC | sel((bytes & 0xFFu) == 0xCBu, PK_EV_CB, 0u), 0u) | sel(pf != 0u, PK_EV_F_LDS, 0u)
             | sel(dispatch, PK_EV_INT, 0u) | sel(!exec && !dispatch, PK_EV_IDLE, 0u);
-        if (exec) PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, op);
-        const uint4 e0 = ucv[di * 3u], e1 = ucv[di * 3u + 1u], e2 = ucv[di * 3u + 2u];
+        if (exec) PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, bytes & 0xFFu);
         const u32 D = e0.x, U = e0.y, K = e0.z, XR = e1.x, XE = e1.y, YR = e1.z, YE = e1.w, AR = e2.x, AE = e2.y,
                   S0 = e2.z, S1 = e2.w;
 
@@ -554,18 +569,38 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         ev |= sel(wr, PK_EV_WR | sel(wr2, PK_EV_WR2, 0u) | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
                       | sel(addr0 >= 0xC000u && addr0 < 0xFE00u, PK_EV_WR_WRAM, sel(addr0 >= 0x8000u && addr0 < 0xA000u, PK_EV_WR_VRAM, 0u)), 0u);
 
+        // ---------------- prefetch the next instruction (LDS-staged ROM or the HRAM mirror) ----------------
+        {
+            const u32 npc = s.pc;
+            const bool fl = rom_staged(s, npc) && (npc & 0x3FFFu) < 0x3FFEu;
+            const u32 la = sel(fl, rom_lds_index(s, npc), 0u);
+            pbytes = __builtin_amdgcn_alignbyte(romw[(la >> 2) + 1u], romw[la >> 2], la & 3u);
+            const bool fh = npc - 0xFF80u < 0x7Du;
+            if (fh) {
+                const u32 q = (npc - 0xFF80u) * PK_WG_ENVS + c.loc;
+                pbytes = lds_hcode[q] | (lds_hcode[q + PK_WG_ENVS] << 8) | (lds_hcode[q + 2u * PK_WG_ENVS] << 16);
+            }
+            const u32 op = pbytes & 0xFFu;
+            const u32 di = sel(op == 0xCBu, 256u + ((pbytes >> 8) & 0xFFu), op);
+            p0 = ucv[di * 3u];
+            p1 = ucv[di * 3u + 1u];
+            p2 = ucv[di * 3u + 2u];
+            pf = sel(fl | fh, 1u, 0u);
+        }
+
         // ---------------- HALT fast-forward, timer, LCD (pyboy mb.tick) ----------------
         const u32 tac = s.tim0 >> 24;
-        const u32 dsh = sel((tac & 3u) == 0u, 10u, sel((tac & 3u) == 1u, 4u, sel((tac & 3u) == 2u, 6u, 8u)));
         // HALT skip-ahead: a halted CPU that nothing can wake before VBlank (no pending or queued
         // interrupt, timer off, STAT HBlank/OAM/LYC interrupts off, frame not rendered) would spend
         // one loop iteration per LCD mode event (3 per scanline) fast-forwarding to it.  Jump to
         // the state right after line 143's mode-0 event in one step instead (exactly the state those
         // iterations would reach: LY, STAT mode and coincidence bit, clock, DIV, watchdog budget),
         // so the VBlank event itself is processed below as usual.
-        {
+        // Both halted-CPU blocks sit behind one `if`: a wave has a halted lane in only a few % of
+        // its iterations, so the others skip their ~50 instructions.
+        if (s.cpu & CPU_HALT) {
             const u32 cpu = s.cpu, stat = bfe8(s.lcd0, 8), ly = bfe8(s.lcd0, 16), nm = s.lcd2 >> 24;
-            const bool cand = (cpu & (CPU_HALT | CPU_QUEUED)) == CPU_HALT && ((cpu >> 8) & (cpu >> 16) & 0x1Fu) == 0u
+            const bool cand = !(cpu & CPU_QUEUED) && ((cpu >> 8) & (cpu >> 16) & 0x1Fu) == 0u
                            && (s.lcd0 & 0x80u) && (stat & 0x68u) == 0u && !(tac & 4u) && !s.render && ly < 143u && nm != 1u && s.clock <= s.target;
             const u32 lines = 143u - ly;
             const u32 vbl = sel(nm == 2u, s.target + 456u * lines, s.target - sel(nm == 3u, 80u, 250u) + 456u * (lines + 1u));
@@ -581,8 +616,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
                 s.lcd0 = (s.lcd0 & 0xFF0000FFu) | (st2 << 8) | (143u << 16);
                 s.lcd2 = (s.lcd2 & 0x00FFFFFFu) | (1u << 24);
             }
-        }
-        if (s.cpu & CPU_HALT) {
+            const u32 dsh = timer_shift(tac);
             const int tb = (int)sel(tac & 4u, ((0x100u - bfe8(s.tim0, 8)) << dsh) - s.timac, 1u << 16);
             const int ta = (int)s.target - (int)s.clock;
             const int mm = ta < tb ? ta : tb;
@@ -591,6 +625,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         u32 irq = 0;
         s.divacc = (s.divacc + cycles) & 0xFFFFu;
         if (tac & 4u) {  // TAC enabled (timer.py Timer.tick)
+            const u32 dsh = timer_shift(tac);
             u32 timac = s.timac + cycles;
             u32 tima = bfe8(s.tim0, 8);
             const u32 mul = timac >> dsh;
