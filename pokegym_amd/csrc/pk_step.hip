@@ -451,27 +451,28 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         const bool rd = bit(D, PK_DB_RD) != 0u, rd2 = bit(D, PK_DB_RD2) != 0u;
         const bool rram = rd & fast_ram(addr0) & fast_ram(addr1);  // addr1 == addr0 for 1-byte reads
         const bool rrom = rd & rom_staged(s, addr0) & rom_staged(s, addr1);
-        u32 m0 = 0, m1 = 0;
+        // each source has its own result registers, merged by OR below: sharing one register
+        // would make the LDS ROM read wait for the image load of other lanes (write-after-write)
+        u32 rm0 = 0, rm1 = 0, om0 = 0, om1 = 0, xm = 0;
         if (rram) {
-            m0 = ld_img(c, fast_phys(addr0));
-            if (rd2) m1 = ld_img(c, fast_phys(addr1));
+            rm0 = ld_img(c, fast_phys(addr0));
+            if (rd2) rm1 = ld_img(c, fast_phys(addr1));
         }
         if (rrom) {
-            m0 = lds_rom[rom_lds_index(s, addr0)];
-            m1 = sel(rd2, (u32)lds_rom[rom_lds_index(s, addr1)], 0u);
+            om0 = lds_rom[rom_lds_index(s, addr0)];
+            om1 = lds_rom[rom_lds_index(s, addr1)];  // == om0 for 1-byte reads, masked below
         }
         if (rd & !rram & !rrom) {  // rare: IO registers (LY, STAT, joypad, ...), SRAM, unstaged ROM
             if (!rd2 & (addr0 >= 0xFF00u) & ((addr0 < 0xFF80u) | (addr0 == 0xFFFFu))) {
-                m0 = io_read(c, s, addr0);
+                xm = io_read(c, s, addr0);
                 ev |= PK_EV_RD_IO;
             } else {
                 const St t = s;
-                const u32 m = pk_read_slow(&A, c.g, c.lane, c.loc, &t, addr0, addr1, rd2 ? 1u : 0u);
-                m0 = m & 0xFFu;
-                m1 = m >> 8;
+                xm = pk_read_slow(&A, c.g, c.lane, c.loc, &t, addr0, addr1, rd2 ? 1u : 0u);
                 ev |= PK_EV_RD_ROMG;
             }
         }
+        const u32 m0 = rm0 | om0 | (xm & 0xFFu), m1 = rm1 | sel(rd2, om1, 0u) | (xm >> 8);
         ev |= sel(rd, PK_EV_RD | sel(rd2, PK_EV_RD2, 0u) | sel(rram, PK_EV_RD_RAM, 0u) | sel(rrom, PK_EV_RD_ROMLDS, 0u)
                       | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
                       | sel(addr0 >= 0xC000u && addr0 < 0xFE00u, PK_EV_RD_WRAM, 0u), 0u);
