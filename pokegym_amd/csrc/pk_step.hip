@@ -431,7 +431,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         ev |= sel(exec, PK_EV_EXEC | sel((bytes & 0xFFu) == 0xCBu, PK_EV_CB, 0u), 0u) | sel(pf != 0u, PK_EV_F_LDS, 0u)
             | sel(dispatch, PK_EV_INT, 0u) | sel(!exec && !dispatch, PK_EV_IDLE, 0u);
         if (exec) PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, bytes & 0xFFu);
-        const u32 D = e0.x, U = e0.y, K = e0.z, XR = e1.x, XE = e1.y, YR = e1.z, YE = e1.w, AR = e2.x, AE = e2.y,
+        const u32 D = e0.x, U = e0.y, K = e0.z, V = e0.w, XR = e1.x, XE = e1.y, YR = e1.z, YE = e1.w, AR = e2.x, AE = e2.y,
                   S0 = e2.z, S1 = e2.w;
 
         // ---------------- operands, condition, memory address ----------------
@@ -446,6 +446,8 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         const u32 asrc = perm(w1, w0, AR) | perm(sp << 16, bytes, AE);
         const u32 addr0 = (asrc + (u32)sfield(D, PK_DB_AOFF, 2)) & 0xFFFFu;
         const u32 addr1 = (addr0 + (u32)sfield(D, PK_DB_ADIR, 2)) & 0xFFFFu;
+        // image offsets of both addresses, shared by the fast read and write paths
+        const u32 o0 = fast_phys(addr0) * PK_LANES + c.lane, o1 = fast_phys(addr1) * PK_LANES + c.lane;
 
         // ---------------- memory reads (m0 at addr0, m1 at addr1) ----------------
         const bool rd = bit(D, PK_DB_RD) != 0u, rd2 = bit(D, PK_DB_RD2) != 0u;
@@ -455,8 +457,8 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         // would make the LDS ROM read wait for the image load of other lanes (write-after-write)
         u32 rm0 = 0, rm1 = 0, om0 = 0, om1 = 0, xm = 0;
         if (rram) {
-            rm0 = ld_img(c, fast_phys(addr0));
-            if (rd2) rm1 = ld_img(c, fast_phys(addr1));
+            rm0 = c.g[o0];
+            if (rd2) rm1 = c.g[o1];
         }
         if (rrom) {
             om0 = lds_rom[rom_lds_index(s, addr0)];
@@ -491,25 +493,25 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         const u32 hsh = 4u + 8u * bit(U, PK_UB_HC16);
         const u32 hf = ((cv >> hsh) & 1u) ^ sub;
         const u32 cf = ((cv >> (hsh + 4u)) & 1u) ^ sub;
-        // logic
-        const u32 lop = (U >> PK_UB_LOP) & 3u;
-        const u32 lres = sel(lop == 0u, X & Y, sel(lop == 1u, X ^ Y, X | Y));
+        // logic: (X & Y) and/or (X ^ Y) under all-ones masks from the microcode (OR = both)
+        const u32 lres = ((X & Y) & (u32)sfield(V, PK_VB_LAND, 1)) | ((X ^ Y) & (u32)sfield(V, PK_VB_LXOR, 1));
         // rotate / shift / swap
         const u32 x8 = X & 0xFFu;
         const bool rdir = bit(U, PK_UB_RDIR) != 0u;
         const u32 b7 = x8 >> 7, rob = sel(rdir, x8 & 1u, b7);
-        const u32 rbin = (U >> PK_UB_RBIN) & 3u;
-        const u32 bin = sel(rbin == 1u, fc, sel(rbin == 2u, rob, sel(rbin == 3u, b7, 0u)));
+        // rotate-in bit: bit RBIN of [0, F.C, rotated-out, bit 7]
+        const u32 bin = ((fc << 1) | (rob << 2) | (b7 << 3)) >> ((U >> PK_UB_RBIN) & 3u) & 1u;
         const u32 rsh = sel(rdir, (x8 >> 1) | (bin << 7), ((x8 << 1) | bin) & 0xFFu);
         const u32 rot = sel(bit(U, PK_UB_SWAP), ((x8 >> 4) | (x8 << 4)) & 0xFFu, rsh);
         // results
-        const u32 r8s = (U >> PK_UB_R8) & 3u;
-        u32 res8 = sel(r8s == 0u, Y, sel(r8s == 1u, r, sel(r8s == 2u, lres, rot))) & 0xFFu;
+        // result8: byte R8 of the pool [Y, adder, logic, rotate] (two v_perm + one shift)
+        const u32 pool = perm(r, Y, 0x0C0C0400u) | perm(rot, lres, 0x04000C0Cu);
+        u32 res8 = (pool >> (V & 31u)) & 0xFFu;
         const u32 hl1 = (hl + (u32)sfield(U, PK_UB_HLINC, 2)) & 0xFFFFu;
         const u32 res16 = sel(bit(U, PK_UB_R16HL), hl1, r & 0xFFFFu);
         // flags: F' = (F & keep) | const | Z | H | C
-        const u32 fcs = (U >> PK_UB_FC) & 3u;
-        const u32 cbit = sel(fcs == 1u, cf, sel(fcs == 2u, rob, sel(fcs == 3u, fc ^ 1u, 0u)));
+        // C: bit FC of [0, adder carry, rotated-out, !F.C]
+        const u32 cbit = ((cf << 1) | (rob << 2) | ((fc ^ 1u) << 3)) >> ((U >> PK_UB_FC) & 3u) & 1u;
         u32 nf = (F & (K >> PK_KB_FKEEP)) | (K >> PK_KB_FCONST) | sel(bit(U, PK_UB_FZ) && res8 == 0u, 0x80u, 0u)
                | ((bit(U, PK_UB_FH) & hf) << 5) | (cbit << 4);
         nf = sel(bit(U, PK_UB_FPOP), m0 & 0xF0u, nf) & 0xFFu;
@@ -554,10 +556,10 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
                 s.npend = 0;
                 ev |= PK_EV_FLUSH;
             }
-            st_img(c, fast_phys(addr0), wv0);
+            c.g[o0] = (u8)wv0;
             hcode_st(c, addr0, wv0);
             if (wr2) {
-                st_img(c, fast_phys(addr1), wv1);
+                c.g[o1] = (u8)wv1;
                 hcode_st(c, addr1, wv1);
             }
         }

@@ -19,7 +19,7 @@
 #include <stdint.h>
 
 // ---- entry layout: 12 dwords (three ds_read_b128) ----
-enum { PK_UE_D = 0, PK_UE_U, PK_UE_K, PK_UE_PAD, PK_UE_XR, PK_UE_XE, PK_UE_YR, PK_UE_YE, PK_UE_AR, PK_UE_AE,
+enum { PK_UE_D = 0, PK_UE_U, PK_UE_K, PK_UE_V, PK_UE_XR, PK_UE_XE, PK_UE_YR, PK_UE_YE, PK_UE_AR, PK_UE_AE,
        PK_UE_S0, PK_UE_S1, PK_UE_WORDS };
 #define PK_UC_ENTRIES 515u
 #define PK_UC_INT 512u    // pseudo-op: interrupt dispatch (push PC, jump to the vector)
@@ -63,6 +63,10 @@ enum { PK_J_NONE = 0, PK_J_XY = 1, PK_J_JR = 2 };  // stored: target = X | Y (op
 #define PK_UB_HC16 8      // H/C from bits 12/16 (else 4/8)
 #define PK_UB_R8 9        // 2 bits result8: 0 Y 1 adder 2 logic 3 rotate
 #define PK_UB_LOP 11      // 2 bits logic: 0 AND 1 XOR 2 OR
+// V word (derived from U by pk_store_uop)
+#define PK_VB_R8SH 0      // 5 bits: result8 byte offset in the [Y, adder, logic, rotate] pool (8 * R8)
+#define PK_VB_LAND 8      // logic result includes X & Y (AND, OR)
+#define PK_VB_LXOR 9      // logic result includes X ^ Y (XOR, OR); OR = AND | XOR
 #define PK_UB_RDIR 13     // rotate right (else left)
 #define PK_UB_RBIN 14     // 2 bits rotate-in bit: 0 zero 1 F.C 2 rotated-out bit 3 bit 7 (SRA)
 #define PK_UB_SWAP 16     // SWAP
@@ -454,7 +458,11 @@ static inline void pk_store_uop(uint32_t* e, PkUop o, bool real) {
     e[PK_UE_D] = o.d & ~(pk_fld(1, PK_DB_ASP) | pk_fld(1, PK_DB_AIMM) | pk_fld(1, PK_DB_AHN) | pk_fld(1, PK_DB_YSP));
     e[PK_UE_U] = o.u & ~63u;
     e[PK_UE_K] = o.k;
-    e[PK_UE_PAD] = 0;
+    // V word: datapath selectors derived from U in the form the kernel consumes in one op
+    {
+        const uint32_t r8 = (o.u >> PK_UB_R8) & 3u, lop = (o.u >> PK_UB_LOP) & 3u;
+        e[PK_UE_V] = pk_fld(8u * r8, PK_VB_R8SH) | pk_fld(lop != 1u ? 1u : 0u, PK_VB_LAND) | pk_fld(lop != 0u ? 1u : 0u, PK_VB_LXOR);
+    }
     e[PK_UE_XR] = xe != PK_PZERO ? PK_PZERO : o.px;
     e[PK_UE_XE] = xe;
     e[PK_UE_YR] = ye != PK_PZERO ? PK_PZERO : o.py;
