@@ -133,6 +133,26 @@ __device__ __forceinline__ u32 slot_base(u32 bank) {
 
 // ---------------------------------------------------------------------------------------------
 // LCD helpers (pyboy lcd.py) — oracle: gbcore.c lcd_set_lcdc
+// Folded line: when no STAT mode interrupt is enabled and the frame is not rendered, a visible
+// line's mode-3 and mode-0 events change nothing but the STAT mode bits, so the mode-2 event
+// schedules the line-end event directly (one LCD event per line instead of three) and marks the
+// line folded.  The mode bits are derived from the clock whenever they are observed (STAT read),
+// and the exact unfolded state is restored before anything else depends on it (STAT write, kernel
+// exit).  The event at the line end sees the same state as in the unfolded sequence except the
+// stored mode 2 instead of 0, which only feeds the mode-change interrupt test (disabled here).
+#define PK_LCD_FOLD (1u << 26)  // lcd2 bit: current line folded (next-mode field = bits 24-25)
+__device__ __forceinline__ u32 lcd_fold_off(const St& s) { return s.clock - (s.target - 456u); }
+__device__ __forceinline__ u32 lcd_fold_mode(u32 off) { return sel(off < 80u, 2u, sel(off < 250u, 3u, 0u)); }
+__device__ __forceinline__ void lcd_unfold(St& s) {
+    if (s.lcd2 & PK_LCD_FOLD) {
+        const u32 off = lcd_fold_off(s);
+        s.lcd0 = (s.lcd0 & ~0x300u) | (lcd_fold_mode(off) << 8);
+        s.target = sel(off < 80u, s.target - 376u, sel(off < 250u, s.target - 206u, s.target));
+        const u32 nm = sel(off < 80u, 3u, sel(off < 250u, 0u, (s.lcd2 >> 24) & 3u));
+        s.lcd2 = (s.lcd2 & 0x00FFFFFFu) | (nm << 24);
+    }
+}
+
 __device__ __forceinline__ void lcd_set_lcdc(St& s, u32 v) {
     s.lcd0 = setb8(s.lcd0, 0, v);
     if (!(v & 0x80u)) {
@@ -181,6 +201,7 @@ __device__ __forceinline__ u32 io_read(const Ctx& c, const St& s, u32 a) {
         const u32 e = (u32)(tab >> (4u * k)) & 15u;
         const u32 w = sel((e >> 2) == 0u, s.lcd0, sel((e >> 2) == 1u, s.lcd1, sel((e >> 2) == 2u, s.lcd2, 0u)));
         v = bfe8(w, 8u * (e & 3u));
+        if (k == 1u && (s.lcd2 & PK_LCD_FOLD)) v = (v & 0xFCu) | lcd_fold_mode(lcd_fold_off(s));
     }
     return v;
 }
@@ -232,7 +253,10 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
             case 0xFF07: s.tim0 = setb8(s.tim0, 24, v & 7u); break;
             case 0xFF0F: s.cpu = setb8(s.cpu, 16, v); break;
             case 0xFF40: lcd_set_lcdc(s, v); break;
-            case 0xFF41: s.lcd0 = setb8(s.lcd0, 8, (bfe8(s.lcd0, 8) & 0x87u) | (v & 0x78u)); break;
+            case 0xFF41:
+                lcd_unfold(s);
+                s.lcd0 = setb8(s.lcd0, 8, (bfe8(s.lcd0, 8) & 0x87u) | (v & 0x78u));
+                break;
             case 0xFF42: s.lcd1 = setb8(s.lcd1, 0, v); break;
             case 0xFF43: s.lcd1 = setb8(s.lcd1, 8, v); break;
             case 0xFF44: break;  // LY is read-only
@@ -602,7 +626,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         // Both halted-CPU blocks sit behind one `if`: a wave has a halted lane in only a few % of
         // its iterations, so the others skip their ~50 instructions.
         if (s.cpu & CPU_HALT) {
-            const u32 cpu = s.cpu, stat = bfe8(s.lcd0, 8), ly = bfe8(s.lcd0, 16), nm = s.lcd2 >> 24;
+            const u32 cpu = s.cpu, stat = bfe8(s.lcd0, 8), ly = bfe8(s.lcd0, 16), nm = (s.lcd2 >> 24) & 3u;
             const bool cand = !(cpu & CPU_QUEUED) && ((cpu >> 8) & (cpu >> 16) & 0x1Fu) == 0u
                            && (s.lcd0 & 0x80u) && (stat & 0x68u) == 0u && !(tac & 4u) && !s.render && ly < 143u && nm != 1u && s.clock <= s.target;
             const u32 lines = 143u - ly;
@@ -645,7 +669,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         const u32 lcdc = s.lcd0 & 0xFFu;
         const bool lcdev = (lcdc & 0x80u) && s.clock >= s.target;
         if (lcdev) {  // lcd.tick mode transition
-            const u32 nm = s.lcd2 >> 24;
+            const u32 nm = (s.lcd2 >> 24) & 3u;
             u32 stat = bfe8(s.lcd0, 8), ly = bfe8(s.lcd0, 16);
             const u32 lyc = s.lcd0 >> 24;
             const bool changed = (stat & 3u) != nm;
@@ -656,16 +680,17 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             s.clock -= sel(wrap && s.clock >= FRAME_CYCLES, FRAME_CYCLES, 0u);
             s.target -= sel(wrap && s.target >= FRAME_CYCLES, FRAME_CYCLES, 0u);
             ly = sel(wrap, 0u, sel(m2 || m1, ly + 1u, ly));
-            s.target += sel(m2, 80u, sel(m3, 170u, sel(m0, 206u, 456u)));
+            const bool fold = m2 && (stat & 0x38u) == 0u && !s.render;  // see lcd_unfold
+            s.target += sel(fold, 456u, sel(m2, 80u, sel(m3, 170u, sel(m0, 206u, 456u))));
             const bool eq = lyc == ly, upd = m2 || m1;
             stat = sel(upd, sel(eq, stat | 4u, stat & 0xFBu), stat);
             irq |= sel(upd && eq && (stat & 0x40u), 2u, 0u);
-            const u32 nnext = sel(m2, 3u, sel(m3, 0u, sel(m0, sel(ly < 143u, 2u, 1u), sel(ly == 153u, 2u, 1u))));
+            const u32 nnext = sel(m2 && !fold, 3u, sel(m3, 0u, sel(m0 || fold, sel(ly < 143u, 2u, 1u), sel(ly == 153u, 2u, 1u))));
             const bool vbl = m1 && ly == 144u;
             irq |= sel(vbl, 1u, 0u);
             s.frame_done |= sel(vbl, 1u, 0u);
             s.lcd0 = (s.lcd0 & 0xFF0000FFu) | (stat << 8) | (ly << 16);
-            s.lcd2 = (s.lcd2 & 0x00FFFFFFu) | (nnext << 24);
+            s.lcd2 = (s.lcd2 & 0x00FFFFFFu) | (nnext << 24) | sel(fold, PK_LCD_FOLD, 0u);
         }
         ev |= sel(lcdev, PK_EV_LCD, 0u);
         {
@@ -709,6 +734,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
     }
 
     if (!active) return;
+    lcd_unfold(s);
     R[PK_R_W0 * np + env] = s.w0;
     R[PK_R_W1 * np + env] = perm(s.w1, s.w1, 0x02030100u);
     R[PK_R_SP * np + env] = s.sp;
