@@ -45,6 +45,8 @@ extern "C" {
 #define PK_F_REWARD 2u          /* reward stack + (72,80,4) obs + reference reset semantics */
 #define PK_F_RELOAD_ON_RESET 4u /* reload the template state on EVERY reset (the reference
                                    reloads only on an env's first reset, environment.py:1241) */
+#define PK_F_HEATMAP 8u         /* keep each env's 444x436 counts_map (environment.py:448, :648-679):
+                                   int32, 774,336 B per env, persists across resets (PK_F_REWARD) */
 
 /* per-env error codes (pk_error_ptr): where the reference's step/reset raises, the env stops
  * (reward 0, state frozen) and reports which exception the reference would have raised */
@@ -58,8 +60,9 @@ extern "C" {
 #define PK_ERR_CAPACITY 7       /* device table full (no reference equivalent) */
 
 /* info telemetry record: the numeric scalars of info["stats"] (57) and info["reward"] (21),
- * environment.py:1621-1704, field order pokegym_amd/info.py FIELDS */
-#define PK_INFO_NFIELDS 78
+ * environment.py:1621-1704, field order pokegym_amd/info.py FIELDS ("coord" is NaN without
+ * PK_F_HEATMAP) */
+#define PK_INFO_NFIELDS 79
 
 typedef struct pk_config {
     uint32_t n_envs;             /* envs on this GPU */
@@ -112,6 +115,8 @@ const uint32_t* pk_error_ptr(pk_handle* h);
 const double* pk_info_ptr(pk_handle* h);
 const uint8_t* pk_info_flag_ptr(pk_handle* h);
 uint32_t pk_info_stride(const pk_handle* h);
+/* device pointer to the int32 [n][444][436] counts_map of every env (PK_F_HEATMAP), null without it */
+int32_t* pk_heatmap_ptr(pk_handle* h);
 
 /* Stream-ordered bulk RAM access for all envs: dense_dev[e * len + i] <-> guest address
  * addr + i of env e.  RAM regions only (0xC000-0xFDFF incl. echo, 0xFF80-0xFFFE). */

@@ -42,7 +42,8 @@ enum {
     RS_NFIELDS
 };
 
-enum { RSD_LAST_REWARD = 0, RSD_TOTAL_HEALING, RSD_LAST_HP, RSD_NFIELDS };
+enum { RSD_LAST_REWARD = 0, RSD_TOTAL_HEALING, RSD_LAST_HP, RSD_COORD /* np.sum(counts_map), survives resets */,
+       RSD_NFIELDS };
 
 // RS_FLAGS bits
 #define RSF_HAS_LAST 1u       // self.last_reward is not None
@@ -63,14 +64,16 @@ enum { RSD_LAST_REWARD = 0, RSD_TOTAL_HEALING, RSD_LAST_HP, RSD_NFIELDS };
 #define PKE_CAPACITY 7u       // device table full (no reference equivalent)
 
 // info telemetry record (environment.py:1621-1704; field order = pokegym_amd/info.py FIELDS)
-#define PK_INFO_NSTATS 57u
+#define PK_INFO_NSTATS 58u
 #define PK_INFO_NREWARD 21u
 #ifndef PK_INFO_NFIELDS
-#define PK_INFO_NFIELDS 78u   // == include/pokegym_amd.h
+#define PK_INFO_NFIELDS 79u   // == include/pokegym_amd.h
 #endif
 static_assert(PK_INFO_NFIELDS == PK_INFO_NSTATS + PK_INFO_NREWARD, "info record layout");
 
 #define PK_CUTC_CAP 64u
+#define PK_HEAT_ROWS 444u     // counts_map = np.zeros((444, 436)) (environment.py:448)
+#define PK_HEAT_COLS 436u
 #define PK_MASK_WORDS 2048u   // 256 rows x 8 words
 #define PK_OBS_H 72u
 #define PK_OBS_W 80u
@@ -94,6 +97,7 @@ struct PkRewardArgs {
     uint8_t* trunc;           // [n] or null
     double* info;             // [PK_INFO_NFIELDS][npad] info record, written where info_flag = 1
     uint8_t* info_flag;       // [n] 1 = this step built the reference's info dict (done or time % 10000 == 0)
+    int32_t* heat;            // [npad][PK_HEAT_ROWS * PK_HEAT_COLS] counts_map, or null (PK_F_HEATMAP off)
     double reward_scale;
     uint32_t n, npad;
     uint32_t cap_log2;        // seen table capacity = 1 << cap_log2

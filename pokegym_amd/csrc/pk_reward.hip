@@ -283,7 +283,16 @@ __global__ void __launch_bounds__(256) pk_reward_kernel(PkRewardArgs A) {
         int gr, gc;
         local_to_global(r, c, map, gr, gc);
         const int last = (int)rs[RS_HEAT_LAST * np + e];
-        if (!(last == (int)map || last == -1) && (gr >= 444 || gc >= 436) && !M.err) M.err = PKE_HEATMAP_INDEX;
+        const bool same = last == (int)map || last == -1;
+        if (!same && (gr >= 444 || gc >= 436) && !M.err) M.err = PKE_HEATMAP_INDEX;
+        // the map itself (PK_F_HEATMAP): +1 on the same map (an out-of-range cell is skipped, the
+        // reference swallows that IndexError, :669-673), -1 at the entry cell of a new map (:676)
+        if (A.heat && !M.err && gr < 444 && gc < 436) {
+            int32_t* cell = A.heat + (size_t)e * (PK_HEAT_ROWS * PK_HEAT_COLS) + (u32)gr * PK_HEAT_COLS + (u32)gc;
+            const int old = *cell, nv = same ? old + 1 : -1;
+            *cell = nv;
+            rsd[RSD_COORD * np + e] = rsd[RSD_COORD * np + e] + (double)(nv - old);
+        }
         rs[RS_HEAT_LAST * np + e] = map;
     }
     // level (:1386-1391)
@@ -571,6 +580,7 @@ __global__ void __launch_bounds__(256) pk_reward_kernel(PkRewardArgs A) {
             put(bag_menu); put(stats_menu); put(pokemon_menu); put(start_menu);
             put((double)used_cut2); put(0.0);       // used_cut, state_loaded_instead_of_resetting_in_game
             put((double)(d7b1 & 1u)); put((double)(3u * ((d7b1 >> 6) & 1u))); put((double)(3u * ((d7b1 >> 7) & 1u)));
+            put(A.heat ? rsd[RSD_COORD * np + e] : __builtin_nan(""));   // coord = np.sum(counts_map)
             // info["reward"]
             put(reward); put((double)max_events); put(level_reward);
             put(0.006 * (double)rs[RS_MAX_OPP * np + e]); put(0.0);

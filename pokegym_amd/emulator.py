@@ -38,7 +38,7 @@ class BatchedEmulator:
     def __init__(self, rom: bytes, n_envs: int, state: bytes | None = None, device: int = 0,
                  frame_skip: int = 24, release_frame: int = 8, render: bool = True,
                  max_episode_steps: int = 20480, reward: bool = False, reload_on_reset: bool = False,
-                 reward_scale: float = 4.0):
+                 reward_scale: float = 4.0, heatmap: bool = False):
         self._L = _native.load()
         if not torch.cuda.is_available():
             raise _native.PkError("no ROCm GPU visible: the HIP path has no CPU fallback")
@@ -57,7 +57,8 @@ class BatchedEmulator:
         cfg.frame_skip = frame_skip
         cfg.release_frame = release_frame
         cfg.flags = ((PK_F_RENDER if render else 0) | (PK_F_REWARD if reward else 0)
-                     | (PK_F_RELOAD_ON_RESET if reload_on_reset else 0))
+                     | (PK_F_RELOAD_ON_RESET if reload_on_reset else 0)
+                     | (_native.PK_F_HEATMAP if (heatmap and reward) else 0))
         cfg.max_episode_steps = max_episode_steps
         cfg.reward_scale = reward_scale
         h = ctypes.c_void_p()
@@ -70,6 +71,7 @@ class BatchedEmulator:
         self.screen = torch.as_tensor(_CudaArray(ptr, (self.n, ROWS, COLS), "|u1"), device=self.device)
         self.obs = None
         self.errors = None
+        self.heatmap = None     # int32 (n, 444, 436) with heatmap=True
         self.info = None        # f64 (PK_INFO_NFIELDS, n) view, field-major (pokegym_amd/info.py FIELDS)
         self.info_flag = None   # u8 (n,): 1 where the last step built the reference's info dict
         if reward:
@@ -83,6 +85,9 @@ class BatchedEmulator:
             self.info = full[:, :self.n]
             self.info_flag = torch.as_tensor(_CudaArray(self._L.pk_info_flag_ptr(self._h), (self.n,), "|u1"),
                                              device=self.device)
+            hp = self._L.pk_heatmap_ptr(self._h)
+            if hp:   # int32 (n, 444, 436) counts_map of every env (environment.py:448, :648-679)
+                self.heatmap = torch.as_tensor(_CudaArray(hp, (self.n,) + _native.HEAT_SHAPE, "<i4"), device=self.device)
         self.rewards = torch.zeros(self.n, dtype=torch.float64, device=self.device)
         self.terminals = torch.zeros(self.n, dtype=torch.uint8, device=self.device)
         self.truncations = torch.zeros(self.n, dtype=torch.uint8, device=self.device)
@@ -190,7 +195,7 @@ class BatchedEmulator:
             self.screen = None
             self.obs = None
             self.errors = None
-            self.info = self.info_flag = None
+            self.info = self.info_flag = self.heatmap = None
             self._L.pk_destroy(self._h)
             self._h = None
 

@@ -20,6 +20,7 @@ import os
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from . import spaces
 from .dist import EpisodeStats, InfoStats, env_rank, shard_range
@@ -46,7 +47,7 @@ class Environment:
         state = _read(state_path if state_path is not None else DEFAULT_STATE)
         self.max_episode_steps, self.reward_scale = max_episode_steps, reward_scale
         self.emu = BatchedEmulator(rom, 1, state=state, device=device, render=True, reward=True,
-                                   max_episode_steps=max_episode_steps, reward_scale=reward_scale)
+                                   max_episode_steps=max_episode_steps, reward_scale=reward_scale, heatmap=True)
         self.observation_space = spaces.observation_space()
         self.action_space = spaces.action_space()
         self.headless = headless
@@ -67,6 +68,9 @@ class Environment:
         self.emu.raise_if_failed(0)
         done = bool(term[0].item())
         info = self.emu.info_dicts([0]).get(0, {})
+        if info:   # "pokemon_exploration_map": self.counts_map (float64 in the reference)
+            info["pokemon_exploration_map"] = self.emu.heatmap[0].cpu().numpy().astype(np.float64)
+            info["stats"]["pokemon_exploration_map"] = info["pokemon_exploration_map"]
         return obs[0].cpu().numpy(), float(rew[0].item()), done, done, info
 
     def render(self):
@@ -81,14 +85,15 @@ class VecEnv:
 
     def __init__(self, num_envs: int, rom_path=None, state_path=None, rom: bytes | None = None, state: bytes | None = None,
                  device: int | None = None, max_episode_steps: int = 20480, reward_scale: float = 4.0,
-                 reload_on_reset: bool = False, env_offset: int = 0, log_interval: int = 128, emulator=None):
+                 reload_on_reset: bool = False, env_offset: int = 0, log_interval: int = 128, emulator=None,
+                 heatmap: bool = False):
         if emulator is None:
             from .emulator import BatchedEmulator
             rom = rom if rom is not None else _read(rom_path or "pokemon_red.gb")
             state = state if state is not None else _read(state_path if state_path is not None else DEFAULT_STATE)
             emulator = BatchedEmulator(rom, num_envs, state=state, device=0 if device is None else device, render=True,
                                        reward=True, max_episode_steps=max_episode_steps, reward_scale=reward_scale,
-                                       reload_on_reset=reload_on_reset)
+                                       reload_on_reset=reload_on_reset, heatmap=heatmap)
         self.emu = emulator
         self.device = emulator.device
         self.num_envs = self.num_agents = num_envs
@@ -128,6 +133,17 @@ class VecEnv:
             if self.info_stats is not None:
                 infos[0].update(self.info_stats.allreduce())
         return obs, rewards, terminals, truncations, infos
+
+    def exploration_map(self, group=None) -> torch.Tensor:
+        """Sum of every env's counts_map over all ranks (int64 (444, 436), RCCL all-reduce) — the
+        aggregate of the reference's per-env info["pokemon_exploration_map"]; needs heatmap=True."""
+        hm = getattr(self.emu, "heatmap", None)
+        if hm is None:
+            raise RuntimeError("VecEnv(heatmap=True) keeps the per-env counts_map")
+        out = hm.sum(dim=0, dtype=torch.int64)
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
+        return out
 
     # PufferLib async API
     def async_reset(self, seed=None):

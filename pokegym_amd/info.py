@@ -8,9 +8,10 @@ info["stats"] and info["reward"] dicts, in the order below (`levels` as its six 
 One deliberate difference: for an empty party the reference's "highest_pokemon_level"
 (max(party_levels), :1672) raises ValueError and kills the env; the record holds 0 instead.
 
-Not in the record: "pokemon_exploration_map" / "coord" (the 444x436 counts_map
-heat map, :648-679), "maps_explored" (np.sum over a Python set — not a number in the reference),
-and the detailed_rewards_* / *_events_aggregate dicts.
+"coord" (np.sum of the 444x436 counts_map heat map, :648-679) is in the record when the heat map
+is kept (PK_F_HEATMAP; NaN otherwise); the map itself ("pokemon_exploration_map") is a device
+array (pk_heatmap_ptr).  Not in the record: "maps_explored" (np.sum over a Python set — not a
+number in the reference) and the detailed_rewards_* / *_events_aggregate dicts.
 """
 from __future__ import annotations
 
@@ -27,6 +28,7 @@ STATS_FIELDS = (
     "bill_saved", "hm_count", "cut_taught", "bill_capt", "cut_coords", "cut_tiles",
     "bag_menu", "stats_menu", "pokemon_menu", "start_menu", "used_cut",
     "state_loaded_instead_of_resetting_in_game", "defeated_fighting_dojo", "got_hitmonlee", "got_hitmonchan",
+    "coord",   # np.sum(counts_map): needs the heat map (PK_F_HEATMAP); NaN in the record without it
 )
 
 REWARD_FIELDS = (
@@ -60,6 +62,10 @@ def info_dict(values) -> dict:
     stats = {}
     for k, v in zip(STATS_FIELDS, values[:ns]):
         if k[:7] == "levels_" and k[7:].isdigit():
+            continue
+        if k == "coord":
+            if v == v:   # not NaN: the heat map is kept
+                stats[k] = float(v)
             continue
         stats[k] = float(v) if k in _FLOAT_STATS else int(v)
     stats["levels"] = [int(v) for v in values[5:11]]

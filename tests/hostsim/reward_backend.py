@@ -30,7 +30,7 @@ class HostsimRewardBackend:
         cfg.rom_len = len(self.rom)
         cfg.state = st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
         cfg.state_len = len(st)
-        cfg.frame_skip, cfg.release_frame, cfg.flags, cfg.max_episode_steps = 0, 8, PK_F_REWARD, max_steps
+        cfg.frame_skip, cfg.release_frame, cfg.flags, cfg.max_episode_steps = 0, 8, PK_F_REWARD | 8, max_steps
         cfg.reward_scale = 4.0
         h = ctypes.c_void_p()
         self._chk(self.L.pk_create(ctypes.byref(cfg), ctypes.byref(h)), "pk_create")
@@ -83,3 +83,8 @@ class HostsimRewardBackend:
         stride = int(self.L.pk_info_stride(h))
         p = ctypes.cast(self.L.pk_info_ptr(h), ctypes.POINTER(ctypes.c_double))
         return [p[i * stride] for i in range(PK_INFO_NFIELDS)]
+
+    def heat(self, h):
+        """The env's counts_map, flat float64 (pk_heatmap_ptr)."""
+        p = ctypes.cast(self.L.pk_heatmap_ptr(h), ctypes.POINTER(ctypes.c_int32))
+        return np.ctypeslib.as_array(p, shape=(444 * 436,)).astype(np.float64)

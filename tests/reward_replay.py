@@ -148,9 +148,18 @@ def check_info(g, got):
     return len(exp)
 
 
+def golden_heat(g, si):
+    """The reference's final counts_map of info sequence si (444*436 flat, float64)."""
+    m = np.zeros(444 * 436, np.float64)
+    k = g["heat_seq"] == si
+    m[g["heat_idx"][k]] = g["heat_val"][k]
+    return m
+
+
 def run_info_replay(backend, base_state: bytes):
     """The info records `backend` emits over the info golden sequences (1-env handle per sequence;
-    a sequence ends at its first error, as the reference raised there)."""
+    a sequence ends at its first error, as the reference raised there).  Also checks each
+    sequence's final counts_map against the reference's when the backend keeps one."""
     g, seqs = info_sequences()
     got = {}
     for si, max_steps, W, H, S, A in seqs:
@@ -172,6 +181,8 @@ def run_info_replay(backend, base_state: bytes):
                     backend.reset(h)
                     if backend.error(h):
                         break
+            if hasattr(backend, "heat"):
+                assert np.array_equal(backend.heat(h), golden_heat(g, si)), ("counts_map", si)
         finally:
             backend.destroy(h)
     return g, got

@@ -20,7 +20,7 @@ class GpuRewardBackend:
     def create(self, state, max_steps):
         from pokegym_amd.emulator import BatchedEmulator
         return BatchedEmulator(self.rom, 1, state=state, frame_skip=0, render=False, reward=True,
-                               max_episode_steps=max_steps)
+                               max_episode_steps=max_steps, heatmap=True)
 
     def destroy(self, h):
         h.close()
@@ -55,6 +55,9 @@ class GpuRewardBackend:
         if not int(h.info_flag[0].item()):
             return None
         return h.info[:, 0].cpu().numpy()
+
+    def heat(self, h):
+        return h.heatmap[0].reshape(-1).cpu().numpy().astype(np.float64)
 
 
 @pytest.mark.gpu
@@ -91,6 +94,7 @@ def test_gpu_environment_info_dict_and_vecenv_info_stats():
     st = infos[2]["stats"]
     assert st["step"] == 3 and len(st["levels"]) == 6 and set(infos[2]["reward"]) >= {"delta", "exploration"}
     assert set(STATS_FIELDS) - set(st) == {f"levels_{i}" for i in range(6)}
+    assert st["coord"] == float(infos[2]["pokemon_exploration_map"].sum()) <= 3.0   # +1 per step, -1 on a map change
     env.close()
     v = VecEnv(64, rom=rom, max_episode_steps=2, log_interval=4)
     v.reset()
@@ -99,6 +103,14 @@ def test_gpu_environment_info_dict_and_vecenv_info_stats():
         out = v.step(torch.zeros(64, dtype=torch.uint8))
     info = out[4][0]
     assert info["info_records"] == 128 and info["stats"]["step"] == 2.0
+    assert info["stats"]["coord"] != info["stats"]["coord"]   # NaN: no heat map kept
+    v.close()
+    v = VecEnv(8, rom=rom, max_episode_steps=2, log_interval=4, heatmap=True)
+    v.reset()
+    for _ in range(4):
+        v.step(torch.zeros(8, dtype=torch.uint8))
+    em = v.exploration_map()
+    assert em.shape == (444, 436) and int(em.sum()) == int(v.emu.heatmap.sum()) <= 8 * 4
     v.close()
 
 

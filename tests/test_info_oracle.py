@@ -5,7 +5,7 @@ import numpy as np
 
 from oracle import reward as R
 from pokegym_amd import info as I
-from reward_replay import check_info, info_sequences, install
+from reward_replay import check_info, golden_heat, info_sequences, install
 
 
 def test_info_fields_match_golden_layout():
@@ -45,3 +45,23 @@ def test_info_dict_shape():
     assert d["stats"]["levels"] == [5, 6, 7, 8, 9, 10] and d["stats"]["step"] == 0
     assert d["reward"]["has_bicycle_in_bag_reward"] == float(I.NFIELDS - 1)
     assert isinstance(d["stats"]["badges"], float) and isinstance(d["stats"]["money"], int)
+
+
+def test_oracle_heat_map_matches_reference():
+    """counts_map (environment.py:648-679) after each sequence: +1 per step on the same map,
+    -1 at the entry cell of a new map, persists across resets."""
+    g, seqs = info_sequences()
+    for si, max_steps, W, H, S, A in seqs:
+        mem = np.zeros(0x10000, np.uint8)
+        bus = R.Bus(mem)
+        st = R.EnvState()
+        install(mem, W[0], H[0])
+        R.reset(st, bus, S[0], reload=lambda: install(mem, W[0], H[0]), max_episode_steps=max_steps)
+        for t in range(1, len(A) + 1):
+            if st.err:
+                break
+            install(mem, W[t], H[t])
+            _, _, done = R.step(st, bus, int(A[t - 1]), S[t])
+            if not st.err and done:
+                R.reset(st, bus, S[t], max_episode_steps=max_steps)
+        assert np.array_equal(st.heat.reshape(-1).astype(np.float64), golden_heat(g, si)), si

@@ -32,6 +32,7 @@ def main():
     bw, bh = replay_gen.load_bank()
     dims = dict(T.MAP_DIMS)
     seqs, ts, vals, errs = [], [], [], []
+    heat_seq, heat_idx, heat_val = [], [], []   # each sequence's final counts_map (nonzero cells)
     for si, (seed, steps, max_steps, allow_err, scen) in enumerate(SEQUENCES):
         W, H, S, A = replay_gen.make_sequence(bw, bh, seed, steps, dims, bool(allow_err), scen, T.MAP_COORD)
         env = ref_env.ReplayEnv(W[0], H[0], S[0])
@@ -57,9 +58,16 @@ def main():
                     env.env.reset(max_episode_steps=max_steps)
                 except Exception:  # noqa: BLE001
                     break
+        cm = np.asarray(env.env.counts_map, np.float64).reshape(-1)
+        nz = np.nonzero(cm)[0]
+        heat_seq += [si] * len(nz)
+        heat_idx += nz.tolist()
+        heat_val += cm[nz].tolist()
     np.savez_compressed(os.path.join(REPO, "tests", "golden", "info_stats.npz"),
                         seqs=np.array(SEQUENCES, np.int64), seq=np.array(seqs, np.int32), t=np.array(ts, np.int32),
-                        values=np.array(vals, np.float64), fields=np.array(list(STATS_FIELDS) + list(REWARD_FIELDS)))
+                        values=np.array(vals, np.float64), fields=np.array(list(STATS_FIELDS) + list(REWARD_FIELDS)),
+                        heat_seq=np.array(heat_seq, np.int32), heat_idx=np.array(heat_idx, np.int32),
+                        heat_val=np.array(heat_val, np.float64))
     print(f"{len(vals)} info records over {len(SEQUENCES)} sequences; step errors: {errs}")
 
 
