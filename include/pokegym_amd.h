@@ -115,6 +115,10 @@ const uint32_t* pk_error_ptr(pk_handle* h);
 const double* pk_info_ptr(pk_handle* h);
 const uint8_t* pk_info_flag_ptr(pk_handle* h);
 uint32_t pk_info_stride(const pk_handle* h);
+/* device pointer to u32 [5][stride] event-monitor bits of the info step (ram_map_leanke.py
+ * monitor_*_events, 130 bits in reward_tables.MONITORS order): the detailed_rewards_* and
+ * *_events_aggregate dicts of the reference's info (environment.py:1706-1808) */
+const uint32_t* pk_info_bits_ptr(pk_handle* h);
 /* device pointer to the int32 [n][444][436] counts_map of every env (PK_F_HEATMAP), null without it */
 int32_t* pk_heatmap_ptr(pk_handle* h);
 

@@ -29,7 +29,7 @@ ROWS, COLS = 144, 160
 EXPORTS = ("pk_create", "pk_destroy", "pk_last_error", "pk_abi_version", "pk_reset", "pk_step",
            "pk_screen_ptr", "pk_num_envs", "pk_peek", "pk_poke", "pk_snapshot", "pk_load_env",
            "pk_last_instr_count", "pk_profile_enable", "pk_profile_read", "pk_obs_ptr", "pk_error_ptr",
-           "pk_get_ram", "pk_set_ram", "pk_info_ptr", "pk_info_flag_ptr", "pk_info_stride", "pk_heatmap_ptr")
+           "pk_get_ram", "pk_set_ram", "pk_info_ptr", "pk_info_flag_ptr", "pk_info_stride", "pk_heatmap_ptr", "pk_info_bits_ptr")
 
 
 class PkConfig(ctypes.Structure):
@@ -104,6 +104,8 @@ def bind_v2(L):
     L.pk_info_stride.restype = ctypes.c_uint32
     L.pk_heatmap_ptr.argtypes = [vp]
     L.pk_heatmap_ptr.restype = vp
+    L.pk_info_bits_ptr.argtypes = [vp]
+    L.pk_info_bits_ptr.restype = vp
     L.pk_get_ram.argtypes = [vp, ctypes.c_uint16, ctypes.c_uint32, vp, vp]
     L.pk_set_ram.argtypes = [vp, ctypes.c_uint16, ctypes.c_uint32, vp, vp]
     L.pk_reset.argtypes = [vp, vp, vp]

@@ -250,6 +250,7 @@ struct pk_handle {
     double* info = nullptr;       // [PK_INFO_NFIELDS][npad]
     uint8_t* info_flag = nullptr; // [npad]
     int32_t* heat = nullptr;      // [npad][444 * 436] (PK_F_HEATMAP)
+    uint32_t* info_bits = nullptr; // [PK_INFO_BITS_WORDS][npad]
     uint32_t cap_log2 = 0;
     double reward_scale = 4.0;
     // profiling: 4 events per profiled step (start, after K1, after K2, after K4+K3)
@@ -280,6 +281,7 @@ const uint32_t* pk_error_ptr(pk_handle* h) { return (h && h->rs) ? h->rs + (size
 const double* pk_info_ptr(pk_handle* h) { return h ? h->info : nullptr; }
 const uint8_t* pk_info_flag_ptr(pk_handle* h) { return h ? h->info_flag : nullptr; }
 int32_t* pk_heatmap_ptr(pk_handle* h) { return h ? h->heat : nullptr; }
+const uint32_t* pk_info_bits_ptr(pk_handle* h) { return h ? h->info_bits : nullptr; }
 uint32_t pk_num_envs(const pk_handle* h) { return h ? h->n : 0; }
 uint32_t pk_info_stride(const pk_handle* h) { return h ? h->npad : 0; }
 
@@ -289,7 +291,7 @@ void pk_destroy(pk_handle* h) {
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     void* ptrs[] = {h->mem, h->regs, h->lat, h->screen, h->rom, h->ucode, h->bank_slot, h->slot_bank, h->t_mem, h->t_regs,
                     h->t_lat, h->t_screen, h->scratch, h->rs, h->rsd, h->seen, h->mask, h->cutc, h->obs, h->reload,
-                    h->info, h->info_flag, h->heat};
+                    h->info, h->info_flag, h->heat, h->info_bits};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete h;
@@ -378,6 +380,7 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
         ALLOC(h->reload, h->npad);
         ALLOC(h->info, (size_t)PK_INFO_NFIELDS * h->npad * 8);
         ALLOC(h->info_flag, h->npad);
+        ALLOC(h->info_bits, (size_t)PK_INFO_BITS_WORDS * h->npad * 4);
         if (h->flags & PK_F_HEATMAP) ALLOC(h->heat, (size_t)h->npad * PK_HEAT_ROWS * PK_HEAT_COLS * 4);
     }
 #undef ALLOC
@@ -419,6 +422,7 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
         if (e == hipSuccess) e = hipMemset(h->obs, 0, (size_t)h->npad * PK_OBS_BYTES);
         if (e == hipSuccess) e = hipMemset(h->info, 0, (size_t)PK_INFO_NFIELDS * h->npad * 8);
         if (e == hipSuccess) e = hipMemset(h->info_flag, 0, h->npad);
+        if (e == hipSuccess) e = hipMemset(h->info_bits, 0, (size_t)PK_INFO_BITS_WORDS * h->npad * 4);
         if (e == hipSuccess && h->heat) e = hipMemset(h->heat, 0, (size_t)h->npad * PK_HEAT_ROWS * PK_HEAT_COLS * 4);
     }
     if (e != hipSuccess) {
@@ -436,7 +440,7 @@ static PkRewardArgs reward_args(pk_handle* h) {
     memset(&r, 0, sizeof r);
     r.mem = h->mem; r.regs = h->regs; r.rs = h->rs; r.rsd = h->rsd; r.seen = h->seen; r.mask = h->mask;
     r.cutc = h->cutc; r.reload = h->reload; r.screen = h->screen; r.obs = h->obs;
-    r.info = h->info; r.info_flag = h->info_flag; r.heat = h->heat;
+    r.info = h->info; r.info_flag = h->info_flag; r.heat = h->heat; r.info_bits = h->info_bits;
     r.reward_scale = h->reward_scale; r.n = h->n; r.npad = h->npad; r.cap_log2 = h->cap_log2;
     r.max_steps = h->max_steps; r.reload_always = (h->flags & PK_F_RELOAD_ON_RESET) ? 1 : 0;
     return r;

@@ -72,6 +72,7 @@ enum { RSD_LAST_REWARD = 0, RSD_TOTAL_HEALING, RSD_LAST_HP, RSD_COORD /* np.sum(
 static_assert(PK_INFO_NFIELDS == PK_INFO_NSTATS + PK_INFO_NREWARD, "info record layout");
 
 #define PK_CUTC_CAP 64u
+#define PK_INFO_BITS_WORDS 5u  // 130 event-monitor bits (ram_map_leanke monitor_*_events), MONITORS order
 #define PK_HEAT_ROWS 444u     // counts_map = np.zeros((444, 436)) (environment.py:448)
 #define PK_HEAT_COLS 436u
 #define PK_MASK_WORDS 2048u   // 256 rows x 8 words
@@ -97,6 +98,7 @@ struct PkRewardArgs {
     uint8_t* trunc;           // [n] or null
     double* info;             // [PK_INFO_NFIELDS][npad] info record, written where info_flag = 1
     uint8_t* info_flag;       // [n] 1 = this step built the reference's info dict (done or time % 10000 == 0)
+    uint32_t* info_bits;      // [PK_INFO_BITS_WORDS][npad] monitor bits of the info record's step
     int32_t* heat;            // [npad][PK_HEAT_ROWS * PK_HEAT_COLS] counts_map, or null (PK_F_HEATMAP off)
     double reward_scale;
     uint32_t n, npad;

@@ -364,12 +364,15 @@ __global__ void __launch_bounds__(256) pk_reward_kernel(PkRewardArgs A) {
     }
     // nine monitor dicts through calculate_event_rewards (:1457-1491, :1201-1219)
     int mon[PK_NMON];
+    u32 mbits[PK_INFO_BITS_WORDS] = {0, 0, 0, 0, 0};   // the monitor bits, for the info dicts
     for (u32 k = 0; k < PK_NMON; k++) {
         int total = 0, cur = 10;
         for (u32 i = pk_mon_start[k]; i < pk_mon_start[k + 1]; i++) {
             const u32 en = pk_mon_ent[i];
             const int w = (int)((en >> 20) & 0xFFu) - 128;
-            const int pts = w * (int)rbit(M, en & 0xFFFFu, (en >> 16) & 0xFu);
+            const u32 b = rbit(M, en & 0xFFFFu, (en >> 16) & 0xFu);
+            mbits[i >> 5] |= b << (i & 31u);
+            const int pts = w * (int)b;
             if (pts > 0) {
                 total += cur * pts;
                 cur += 2;
@@ -589,6 +592,8 @@ __global__ void __launch_bounds__(256) pk_reward_kernel(PkRewardArgs A) {
             put(scale * (double)seen_cnt); put(scale * (double)caught_cnt); put(scale * (double)moves_cnt);
             put((double)cut_rew); put(tree); put((double)dojo);
             for (u32 t = 0; t < 5u; t++) put(((flags >> (8u + t)) & 1u) ? 20.0 : 0.0);
+            if (A.info_bits)
+                for (u32 j = 0; j < PK_INFO_BITS_WORDS; j++) A.info_bits[(size_t)j * np + e] = mbits[j];
             if (A.info_flag) A.info_flag[e] = 1;
         }
     }

@@ -15,7 +15,7 @@ import numpy as np
 import torch
 
 from . import _native
-from .info import NFIELDS, info_dict
+from .info import NFIELDS, event_dicts, info_dict
 from ._native import (COLS, ERR_EXCEPTIONS, OBS_SHAPE, PK_F_RELOAD_ON_RESET, PK_F_RENDER, PK_F_REWARD, ROWS,
                       STATE_V9_BYTES, check)
 
@@ -72,6 +72,7 @@ class BatchedEmulator:
         self.obs = None
         self.errors = None
         self.heatmap = None     # int32 (n, 444, 436) with heatmap=True
+        self.info_bits = None
         self.info = None        # f64 (PK_INFO_NFIELDS, n) view, field-major (pokegym_amd/info.py FIELDS)
         self.info_flag = None   # u8 (n,): 1 where the last step built the reference's info dict
         if reward:
@@ -83,6 +84,8 @@ class BatchedEmulator:
             full = torch.as_tensor(_CudaArray(self._L.pk_info_ptr(self._h), (NFIELDS, stride), "<f8"),
                                    device=self.device)
             self.info = full[:, :self.n]
+            bits = torch.as_tensor(_CudaArray(self._L.pk_info_bits_ptr(self._h), (5, stride), "<i4"), device=self.device)
+            self.info_bits = bits[:, :self.n]   # event-monitor bits (int32 words; pokegym_amd/info.py event_dicts)
             self.info_flag = torch.as_tensor(_CudaArray(self._L.pk_info_flag_ptr(self._h), (self.n,), "|u1"),
                                              device=self.device)
             hp = self._L.pk_heatmap_ptr(self._h)
@@ -140,7 +143,8 @@ class BatchedEmulator:
         if not ids.numel():
             return {}
         rec = self.info[:, ids].t().cpu().numpy()
-        return {int(e): info_dict(r) for e, r in zip(ids.tolist(), rec)}
+        bits = (self.info_bits[:, ids].t().cpu().numpy().astype(np.int64) & 0xFFFFFFFF)
+        return {int(e): {**info_dict(r), **event_dicts(b)} for e, r, b in zip(ids.tolist(), rec, bits)}
 
     # -- bulk RAM views (stream-ordered) ------------------------------------------------
     def get_ram(self, addr: int, length: int, out: torch.Tensor | None = None) -> torch.Tensor:
@@ -195,7 +199,7 @@ class BatchedEmulator:
             self.screen = None
             self.obs = None
             self.errors = None
-            self.info = self.info_flag = self.heatmap = None
+            self.info = self.info_flag = self.heatmap = self.info_bits = None
             self._L.pk_destroy(self._h)
             self._h = None
 

@@ -11,7 +11,8 @@ One deliberate difference: for an empty party the reference's "highest_pokemon_l
 "coord" (np.sum of the 444x436 counts_map heat map, :648-679) is in the record when the heat map
 is kept (PK_F_HEATMAP; NaN otherwise); the map itself ("pokemon_exploration_map") is a device
 array (pk_heatmap_ptr).  Not in the record: "maps_explored" (np.sum over a Python set — not a
-number in the reference) and the detailed_rewards_* / *_events_aggregate dicts.
+number in the reference).  The detailed_rewards_* / *_events_aggregate dicts come from the 130
+event-monitor bits K4 stores beside the record (pk_info_bits_ptr, event_dicts below).
 """
 from __future__ import annotations
 
@@ -71,3 +72,39 @@ def info_dict(values) -> dict:
     stats["levels"] = [int(v) for v in values[5:11]]
     reward = {k: float(v) for k, v in zip(REWARD_FIELDS, values[ns:])}
     return {"stats": stats, "reward": reward}
+
+
+# ---- event-monitor dicts (environment.py:1706-1808): K4 emits the 130 monitor bits ----------
+def _monitors():
+    from . import reward_tables as T
+    return T.MONITORS
+
+
+def event_values(bits) -> list:
+    """Monitor bits (u32 words, reward_tables.MONITORS order) -> weight * bit per entry."""
+    out, i = [], 0
+    for ents in _monitors().values():
+        for _, _, _, wgt in ents:
+            out.append(wgt * ((int(bits[i >> 5]) >> (i & 31)) & 1))
+            i += 1
+    return out
+
+
+def detailed(v: int, base: int = 10, inc: int = 2, mult: int = 1):
+    """calculate_event_rewards_detailed (environment.py:1221-1231) for one event value."""
+    return base + v * inc * mult if v > 0 else v * inc * mult
+
+
+def event_dicts(bits) -> dict:
+    """The reference info dict's detailed_rewards_* and *_events_aggregate entries."""
+    vals = iter(event_values(bits))
+    agg = {k: {name: next(vals) for name, _, _, _ in ents} for k, ents in _monitors().items()}
+    det = {k: {n: detailed(v) for n, v in d.items()} for k, d in agg.items()}
+    return {
+        "detailed_rewards_silph_co": det["silph_co"], "detailed_rewards_dojo": det["dojo"],
+        "detailed_rewards_hideout": det["hideout"], "detailed_rewards_poke_tower": det["poke_tower"],
+        "detailed_rewards_gyms": {f"gym_{g}_detailed_rewards": det[f"gym{g}"] for g in range(3, 8)},
+        "silph_co_events_aggregate": agg["silph_co"], "dojo_events_aggregate": agg["dojo"],
+        "hideout_events_aggregate": agg["hideout"], "poke_tower_events_aggregate": agg["poke_tower"],
+        "gym_events": {f"gym_{g}_events": agg[f"gym{g}"] for g in range(3, 8)},
+    }

@@ -88,3 +88,10 @@ class HostsimRewardBackend:
         """The env's counts_map, flat float64 (pk_heatmap_ptr)."""
         p = ctypes.cast(self.L.pk_heatmap_ptr(h), ctypes.POINTER(ctypes.c_int32))
         return np.ctypeslib.as_array(p, shape=(444 * 436,)).astype(np.float64)
+
+    def events(self, h):
+        """The info step's 130 monitor values (pk_info_bits_ptr -> pokegym_amd.info.event_values)."""
+        from pokegym_amd.info import event_values
+        stride = int(self.L.pk_info_stride(h))
+        p = ctypes.cast(self.L.pk_info_bits_ptr(h), ctypes.POINTER(ctypes.c_uint32))
+        return event_values([p[j * stride] for j in range(5)])

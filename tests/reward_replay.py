@@ -156,12 +156,28 @@ def golden_heat(g, si):
     return m
 
 
+def check_events(g, got):
+    """got: {(seq, t): 130 monitor values (weight * bit)} -> equals the reference's aggregates."""
+    exp = {(int(s), int(t)): v for s, t, v in zip(g["seq"], g["t"], g["event_values"])}
+    assert sorted(got) == sorted(exp)
+    for k, v in exp.items():
+        assert [float(x) for x in got[k]] == v.tolist(), k
+
+
+class _Records(dict):
+    """{(seq, t): info record}; .events = {(seq, t): monitor values}."""
+
+    def __init__(self):
+        super().__init__()
+        self.events = {}
+
+
 def run_info_replay(backend, base_state: bytes):
     """The info records `backend` emits over the info golden sequences (1-env handle per sequence;
     a sequence ends at its first error, as the reference raised there).  Also checks each
     sequence's final counts_map against the reference's when the backend keeps one."""
     g, seqs = info_sequences()
-    got = {}
+    got = _Records()
     for si, max_steps, W, H, S, A in seqs:
         h = backend.create(template_state(base_state, W[0], H[0], S[0]), max_steps)
         try:
@@ -177,6 +193,7 @@ def run_info_replay(backend, base_state: bytes):
                 rec = backend.info(h)
                 if rec is not None:
                     got[(si, t)] = np.asarray(rec, np.float64)
+                    got.events[(si, t)] = backend.events(h)
                 if d:
                     backend.reset(h)
                     if backend.error(h):

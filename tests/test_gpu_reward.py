@@ -56,6 +56,10 @@ class GpuRewardBackend:
             return None
         return h.info[:, 0].cpu().numpy()
 
+    def events(self, h):
+        from pokegym_amd.info import event_values
+        return event_values((h.info_bits[:, 0].cpu().numpy().astype(np.int64) & 0xFFFFFFFF).tolist())
+
     def heat(self, h):
         return h.heatmap[0].reshape(-1).cpu().numpy().astype(np.float64)
 
@@ -71,11 +75,12 @@ def test_gpu_reward_kernels_match_reference_replay():
 @pytest.mark.gpu
 def test_gpu_info_record_matches_reference():
     """K4's info telemetry record (pk_info_ptr) against the reference's info dicts."""
-    from reward_replay import check_info, run_info_replay
+    from reward_replay import check_events, check_info, run_info_replay
     from pokegym_amd.testrom.game import game_rom
     base = open(os.path.join(REPO, "pokegym_amd", "states", "Bulbasaur.state"), "rb").read()
     g, got = run_info_replay(GpuRewardBackend(game_rom()), base)
     assert check_info(g, got) > 100
+    check_events(g, got.events)
 
 
 @pytest.mark.gpu
@@ -92,6 +97,7 @@ def test_gpu_environment_info_dict_and_vecenv_info_stats():
     infos = [env.step(0)[4] for _ in range(3)]
     assert infos[0] == {} and infos[1] == {}
     st = infos[2]["stats"]
+    assert set(infos[2]["gym_events"]) == {f"gym_{g}_events" for g in range(3, 8)} and "dojo_events_aggregate" in infos[2]
     assert st["step"] == 3 and len(st["levels"]) == 6 and set(infos[2]["reward"]) >= {"delta", "exploration"}
     assert set(STATS_FIELDS) - set(st) == {f"levels_{i}" for i in range(6)}
     assert st["coord"] == float(infos[2]["pokemon_exploration_map"].sum()) <= 3.0   # +1 per step, -1 on a map change

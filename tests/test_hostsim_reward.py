@@ -26,8 +26,9 @@ def test_hostsim_reward_kernels_match_reference_replay():
 def test_hostsim_info_record_matches_reference():
     """K4's info telemetry (pk_info_ptr / pk_info_flag_ptr) against the reference's info dicts."""
     from reward_backend import HostsimRewardBackend
-    from reward_replay import check_info, run_info_replay
+    from reward_replay import check_events, check_info, run_info_replay
     from pokegym_amd.testrom.game import game_rom
     base = open(os.path.join(HERE, "..", "pokegym_amd", "states", "Bulbasaur.state"), "rb").read()
     g, got = run_info_replay(HostsimRewardBackend(game_rom()), base)
     assert check_info(g, got) > 100
+    check_events(g, got.events)

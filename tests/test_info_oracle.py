@@ -5,7 +5,7 @@ import numpy as np
 
 from oracle import reward as R
 from pokegym_amd import info as I
-from reward_replay import check_info, golden_heat, info_sequences, install
+from reward_replay import check_events, check_info, golden_heat, info_sequences, install
 
 
 def test_info_fields_match_golden_layout():
@@ -16,7 +16,7 @@ def test_info_fields_match_golden_layout():
 
 def test_oracle_info_matches_reference():
     g, seqs = info_sequences()
-    got = {}
+    got, events = {}, {}
     for si, max_steps, W, H, S, A in seqs:
         mem = np.zeros(0x10000, np.uint8)
         bus = R.Bus(mem)
@@ -32,11 +32,32 @@ def test_oracle_info_matches_reference():
                 break
             if st.info is not None:
                 got[(si, t)] = st.info
+                events[(si, t)] = st.info_events
             if done:
                 R.reset(st, bus, S[t], max_episode_steps=max_steps)
                 if st.err:
                     break
     assert check_info(g, got) > 100
+    check_events(g, events)
+
+
+def test_event_dicts_from_bits():
+    """info.event_dicts rebuilds the reference's nested dicts from the monitor bits."""
+    g, _ = info_sequences()
+    for row in range(len(g["event_values"])):
+        vals = g["event_values"][row].astype(int).tolist()
+        bits = [0] * 5
+        for i, v in enumerate(vals):
+            bits[i >> 5] |= (1 if v != 0 else 0) << (i & 31)
+        d = I.event_dicts(bits)
+        flat = [v for k in ("dojo_events_aggregate", "silph_co_events_aggregate", "hideout_events_aggregate",
+                            "poke_tower_events_aggregate") for v in d[k].values()]
+        flat += [v for gk in range(3, 8) for v in d["gym_events"][f"gym_{gk}_events"].values()]
+        assert flat == vals
+        det = [v for k in ("detailed_rewards_dojo", "detailed_rewards_silph_co", "detailed_rewards_hideout",
+                           "detailed_rewards_poke_tower") for v in d[k].values()]
+        det += [v for gk in range(3, 8) for v in d["detailed_rewards_gyms"][f"gym_{gk}_detailed_rewards"].values()]
+        assert det == g["detail_values"][row].tolist()
 
 
 def test_info_dict_shape():

@@ -24,6 +24,12 @@ import replay_gen  # noqa: E402
 from pokegym_amd import reward_tables as T  # noqa: E402
 from pokegym_amd.info import REWARD_FIELDS, STATS_FIELDS, reference_value  # noqa: E402
 
+# the reference info dict's event-monitor entries, in the order of reward_tables.MONITORS
+EVENT_KEYS = ("dojo_events_aggregate", "silph_co_events_aggregate", "hideout_events_aggregate",
+              "poke_tower_events_aggregate")
+DETAIL_KEYS = ("detailed_rewards_dojo", "detailed_rewards_silph_co", "detailed_rewards_hideout",
+               "detailed_rewards_poke_tower")
+
 # (seed, steps, max_episode_steps, allow_errors, scenario)
 SEQUENCES = [(500 + s, 24, 3 + (s % 6), 0, (0, 0, 1, 2, 3, 4)[s % 6]) for s in range(64)]
 
@@ -33,6 +39,7 @@ def main():
     dims = dict(T.MAP_DIMS)
     seqs, ts, vals, errs = [], [], [], []
     heat_seq, heat_idx, heat_val = [], [], []   # each sequence's final counts_map (nonzero cells)
+    ev_names, ev_vals, det_vals = None, [], []     # the nine *_events_aggregate / detailed_rewards_* dicts
     for si, (seed, steps, max_steps, allow_err, scen) in enumerate(SEQUENCES):
         W, H, S, A = replay_gen.make_sequence(bw, bh, seed, steps, dims, bool(allow_err), scen, T.MAP_COORD)
         env = ref_env.ReplayEnv(W[0], H[0], S[0])
@@ -53,6 +60,14 @@ def main():
                 seqs.append(si)
                 ts.append(t)
                 vals.append(row)
+                agg = [info[k] for k in EVENT_KEYS[:4]] + [info["gym_events"][f"gym_{g}_events"] for g in range(3, 8)]
+                det = [info[k] for k in DETAIL_KEYS[:4]] + [info["detailed_rewards_gyms"][f"gym_{g}_detailed_rewards"]
+                                                            for g in range(3, 8)]
+                names = [f"{i}:{n}" for i, d in enumerate(agg) for n in d]
+                assert ev_names is None or names == ev_names
+                ev_names = names
+                ev_vals.append([float(v) for d in agg for v in d.values()])
+                det_vals.append([float(v) for d in det for v in d.values()])
             if done:
                 try:
                     env.env.reset(max_episode_steps=max_steps)
@@ -67,7 +82,8 @@ def main():
                         seqs=np.array(SEQUENCES, np.int64), seq=np.array(seqs, np.int32), t=np.array(ts, np.int32),
                         values=np.array(vals, np.float64), fields=np.array(list(STATS_FIELDS) + list(REWARD_FIELDS)),
                         heat_seq=np.array(heat_seq, np.int32), heat_idx=np.array(heat_idx, np.int32),
-                        heat_val=np.array(heat_val, np.float64))
+                        heat_val=np.array(heat_val, np.float64), event_names=np.array(ev_names),
+                        event_values=np.array(ev_vals, np.float64), detail_values=np.array(det_vals, np.float64))
     print(f"{len(vals)} info records over {len(SEQUENCES)} sequences; step errors: {errs}")
 
 
