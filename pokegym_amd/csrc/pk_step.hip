@@ -73,6 +73,8 @@ __shared__ u8 lds_hcode[128u * PK_WG_ENVS];
 // ---------------------------------------------------------------------------------------------
 // branch-free helpers: arguments are evaluated unconditionally, so ?: on them is a v_cndmask
 __device__ __forceinline__ u32 sel(bool c, u32 a, u32 b) { return c ? a : b; }
+// rare-path hint: the block is laid out away from the hot instruction stream (instruction fetch)
+#define PK_RARE(x) __builtin_expect(!!(x), 0)
 // TIMA input clock divider as a shift: TAC & 3 = 0/1/2/3 -> 1024/16/64/256 cycles
 __device__ __forceinline__ u32 timer_shift(u32 tac) { return (0x0806040Au >> (8u * (tac & 3u))) & 0xFFu; }
 __device__ __forceinline__ u32 bit(u32 w, int pos) { return (w >> pos) & 1u; }
@@ -403,7 +405,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         const u32 pend = (cpu0 >> 8) & (cpu0 >> 16) & 0x1Fu;
         bool exec = true, doint = false, dispatch = false;
         u32 pc = s.pc, intflag = 0;
-        if ((cpu0 & (CPU_CRASH | CPU_HALT | CPU_QUEUED)) | pend) {
+        if (PK_RARE((cpu0 & (CPU_CRASH | CPU_HALT | CPU_QUEUED)) | pend)) {
             pf = 0;
             const bool crashed = (cpu0 & CPU_CRASH) != 0u;
             const bool halted = (cpu0 & CPU_HALT) != 0u;
@@ -420,13 +422,13 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         // ---------------- fetch + microcode entry (prefetched, or here when pf = 0) ----------------
         u32 bytes = pbytes;
         uint4 e0 = p0, e1 = p1, e2 = p2;
-        if (!pf) {
+        if (PK_RARE(!pf)) {
             const bool flds = rom_staged(s, pc) && (pc & 0x3FFFu) < 0x3FFEu;
             const u32 la = sel(flds, rom_lds_index(s, pc), 0u);
             bytes = __builtin_amdgcn_alignbyte(romw[(la >> 2) + 1u], romw[la >> 2], la & 3u);
             // code outside the staged ROM (rare): RAM code such as the HRAM OAM-DMA wait loop reads the
             // image (three loads when pc..pc+2 stay in one 512-byte block of plain RAM), else the bus
-            if (exec & !flds) {
+            if (PK_RARE(exec & !flds)) {
                 if (pc - 0xFF80u < 0x7Du) {  // pc..pc+2 inside HRAM: the LDS mirror
                     const u32 q = (pc - 0xFF80u) * PK_WG_ENVS + c.loc;
                     bytes = lds_hcode[q] | (lds_hcode[q + PK_WG_ENVS] << 8) | (lds_hcode[q + 2u * PK_WG_ENVS] << 16);
@@ -488,7 +490,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             om0 = lds_rom[rom_lds_index(s, addr0)];
             om1 = lds_rom[rom_lds_index(s, addr1)];  // == om0 for 1-byte reads, masked below
         }
-        if (rd & !rram & !rrom) {  // rare: IO registers (LY, STAT, joypad, ...), SRAM, unstaged ROM
+        if (PK_RARE(rd & !rram & !rrom)) {  // rare: IO registers (LY, STAT, joypad, ...), SRAM, unstaged ROM
             if (!rd2 & (addr0 >= 0xFF00u) & ((addr0 < 0xFF80u) | (addr0 == 0xFFFFu))) {
                 xm = io_read(c, s, addr0);
                 ev |= PK_EV_RD_IO;
@@ -539,7 +541,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         u32 nf = (F & (K >> PK_KB_FKEEP)) | (K >> PK_KB_FCONST) | sel(bit(U, PK_UB_FZ) && res8 == 0u, 0x80u, 0u)
                | ((bit(U, PK_UB_FH) & hf) << 5) | (cbit << 4);
         nf = sel(bit(U, PK_UB_FPOP), m0 & 0xF0u, nf) & 0xFFu;
-        if (bit(D, PK_DB_DAA)) {  // DAA (opcodes.py DAA_27), rare
+        if (PK_RARE(bit(D, PK_DB_DAA))) {  // DAA (opcodes.py DAA_27), rare
             const u32 a = w1 >> 24;
             u32 corr = sel(F & 0x20u, 0x06u, 0u) | sel(F & 0x10u, 0x60u, 0u);
             corr |= sel(F & 0x40u, 0u, sel((a & 0x0Fu) > 0x09u, 0x06u, 0u) | sel(a > 0x99u, 0x60u, 0u));
@@ -575,7 +577,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         const bool wram = wr & fast_ram(addr0) & fast_ram(addr1);
         if (wram) {
             // VRAM / OAM change while rendered lines are pending: rasterise them first (rare)
-            if ((s.npend != 0u) & (vram_or_oam(addr0) | (wr2 & vram_or_oam(addr1)))) {
+            if (PK_RARE((s.npend != 0u) & (vram_or_oam(addr0) | (wr2 & vram_or_oam(addr1))))) {
                 flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, env, c.gid);
                 s.npend = 0;
                 ev |= PK_EV_FLUSH;
@@ -587,7 +589,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
                 hcode_st(c, addr1, wv1);
             }
         }
-        if (wr & !wram) {  // rare: IO registers / MBC / SRAM / OAM DMA / IE
+        if (PK_RARE(wr & !wram)) {  // rare: IO registers / MBC / SRAM / OAM DMA / IE
             St t = s;
             pk_write_slow(&A, c.g, c.lane, c.loc, env, c.gid, &t, addr0, wv0, addr1, wv1, wr2 ? 1u : 0u);
             s = t;
@@ -625,7 +627,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         // so the VBlank event itself is processed below as usual.
         // Both halted-CPU blocks sit behind one `if`: a wave has a halted lane in only a few % of
         // its iterations, so the others skip their ~50 instructions.
-        if (s.cpu & CPU_HALT) {
+        if (PK_RARE(s.cpu & CPU_HALT)) {
             const u32 cpu = s.cpu, stat = bfe8(s.lcd0, 8), ly = bfe8(s.lcd0, 16), nm = (s.lcd2 >> 24) & 3u;
             const bool cand = !(cpu & CPU_QUEUED) && ((cpu >> 8) & (cpu >> 16) & 0x1Fu) == 0u
                            && (s.lcd0 & 0x80u) && (stat & 0x68u) == 0u && !(tac & 4u) && !s.render && ly < 143u && nm != 1u && s.clock <= s.target;
@@ -697,7 +699,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             // latch this scanline's registers at its mode-0 event in the rendered frame; K2 (or
             // flush_lines) rasterises it later
             const u32 ly = bfe8(s.lcd0, 16);
-            if (lcdev && s.render && (s.lcd0 & 0x300u) == 0u && ly < PK_ROWS) {
+            if (PK_RARE(lcdev && s.render && (s.lcd0 & 0x300u) == 0u && ly < PK_ROWS)) {
                 const u32 wy = bfe8(s.lcd1, 16), wx = bfe8(s.lcd1, 24);
                 int lw = (int)bfe8(s.misc, 16) - 1;
                 if ((lcdc & 0x20u) && wy <= ly && (int)wx - 7 < (int)PK_COLS) lw += 1;
@@ -710,7 +712,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
                 s.npend += 1u;
             }
         }
-        if (!(lcdc & 0x80u) && s.clock >= FRAME_CYCLES) {  // LCD off: the frame ends on the clock alone
+        if (PK_RARE(!(lcdc & 0x80u) && s.clock >= FRAME_CYCLES)) {  // LCD off: the frame ends on the clock alone
             s.frame_done = 1u;
             s.clock %= FRAME_CYCLES;
             s.blank |= s.render;
@@ -720,7 +722,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         s.frame_done |= sel(budget > 16u * FRAME_CYCLES, 1u, 0u);
         ev |= sel(s.frame_done != 0u, PK_EV_FRAME, 0u);
         PK_ITER(env, ev);
-        if (s.frame_done) {
+        if (PK_RARE(s.frame_done)) {
             s.frame_done = 0;
             budget = 0;
             frame += 1u;

@@ -16,7 +16,9 @@ per GPU and build each rank's shard with `make_sharded_vecenv`.
 """
 from __future__ import annotations
 
+import io
 import os
+import random
 
 import numpy as np
 import torch
@@ -51,6 +53,31 @@ class Environment:
         self.observation_space = spaces.observation_space()
         self.action_space = spaces.action_space()
         self.headless = headless
+        self.initial_states = [io.BytesIO(state)]   # environment.py:119-120 (the template state)
+        self.pokemon_center_save_states = []
+
+    # -- savestates (environment.py:208-227): PyBoy v9 images of the device state --------------
+    def save_state(self):
+        """environment.py:208-213: append the current machine state (v9 savestate) to
+        pokemon_center_save_states."""
+        self.pokemon_center_save_states.append(io.BytesIO(self.emu.snapshot(0)))
+
+    def load_pokemon_center_state(self):
+        return self.pokemon_center_save_states[len(self.pokemon_center_save_states) - 1]
+
+    def load_last_state(self):
+        return self.initial_states[len(self.initial_states) - 1]
+
+    def load_first_state(self):
+        return self.initial_states[0]
+
+    def load_random_state(self):
+        return self.initial_states[random.randint(0, len(self.initial_states) - 1)]
+
+    def load_pyboy_state(self, state):
+        """pyboy_binding.py:59-69 load_pyboy_state: install a v9 savestate (bytes or file object)."""
+        data = state.getvalue() if hasattr(state, "getvalue") else bytes(state)
+        self.emu.load_env(0, data)
 
     def reset(self, seed=None, options=None, max_episode_steps=None, reward_scale=None):
         """environment.py:1233-1334 (seeding is not supported, as in the reference)."""
@@ -133,6 +160,14 @@ class VecEnv:
             if self.info_stats is not None:
                 infos[0].update(self.info_stats.allreduce())
         return obs, rewards, terminals, truncations, infos
+
+    def save_state(self, env: int) -> bytes:
+        """PyBoy v9 savestate of one env (pk_snapshot; environment.py:208-213 per env)."""
+        return self.emu.snapshot(env)
+
+    def load_state(self, env: int, state: bytes):
+        """Install a v9 savestate into one env (pk_load_env; pyboy_binding.py:59-69)."""
+        self.emu.load_env(env, state)
 
     def exploration_map(self, group=None) -> torch.Tensor:
         """Sum of every env's counts_map over all ranks (int64 (444, 436), RCCL all-reduce) — the

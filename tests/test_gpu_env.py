@@ -37,3 +37,26 @@ def test_vecenv_steps_and_autoresets():
     assert term.all()
     assert infos and infos[0]["episodes"] == 256
     env.close()
+
+
+@pytest.mark.gpu
+def test_environment_savestates_round_trip(tmp_path):
+    """environment.py:208-227 save_state / load_*_state through the device v9 export/import."""
+    from pokegym_amd.env import Environment
+    from pokegym_amd.testrom.game import game_rom
+    env = Environment(rom_path=game_rom(), max_episode_steps=100)
+    env.reset()
+    for t in range(3):
+        env.step(t % 8)
+    env.save_state()
+    saved = env.load_pokemon_center_state().getvalue()
+    ram0 = env.emu.get_ram(0xC000, 8192)[0].cpu().numpy().copy()
+    env.emu.poke(0, 0xC100, bytes([ram0[0x100] ^ 0xFF, ram0[0x101] ^ 0xFF]))
+    env.step(3)
+    env.emu.poke(0, 0xC100, bytes([ram0[0x100] ^ 0xFF]))
+    assert not np.array_equal(env.emu.get_ram(0xC000, 8192)[0].cpu().numpy(), ram0)
+    env.load_pyboy_state(env.load_pokemon_center_state())
+    assert np.array_equal(env.emu.get_ram(0xC000, 8192)[0].cpu().numpy(), ram0)
+    assert env.emu.snapshot(0) == saved
+    assert len(env.load_first_state().getvalue()) == len(saved)
+    env.close()
