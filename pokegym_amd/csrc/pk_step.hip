@@ -577,10 +577,13 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         const bool wram = wr & fast_ram(addr0) & fast_ram(addr1);
         if (wram) {
             // VRAM / OAM change while rendered lines are pending: rasterise them first (rare)
-            if (PK_RARE((s.npend != 0u) & (vram_or_oam(addr0) | (wr2 & vram_or_oam(addr1))))) {
-                flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, env, c.gid);
-                s.npend = 0;
-                ev |= PK_EV_FLUSH;
+            // (lines are pending only in the rendered frame: test that first, alone)
+            if (PK_RARE(s.npend != 0u)) {
+                if (vram_or_oam(addr0) | (wr2 & vram_or_oam(addr1))) {
+                    flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, env, c.gid);
+                    s.npend = 0;
+                    ev |= PK_EV_FLUSH;
+                }
             }
             c.g[o0] = (u8)wv0;
             hcode_st(c, addr0, wv0);
@@ -653,7 +656,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         }
         u32 irq = 0;
         s.divacc = (s.divacc + cycles) & 0xFFFFu;
-        if (tac & 4u) {  // TAC enabled (timer.py Timer.tick)
+        if (PK_RARE(tac & 4u)) {  // TAC enabled (timer.py Timer.tick)
             const u32 dsh = timer_shift(tac);
             u32 timac = s.timac + cycles;
             u32 tima = bfe8(s.tim0, 8);
@@ -719,10 +722,9 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         }
         s.cpu |= irq << 16;
         budget += cycles + 1u;
-        s.frame_done |= sel(budget > 16u * FRAME_CYCLES, 1u, 0u);
-        ev |= sel(s.frame_done != 0u, PK_EV_FRAME, 0u);
+        ev |= sel(s.frame_done != 0u || budget > 16u * FRAME_CYCLES, PK_EV_FRAME, 0u);
         PK_ITER(env, ev);
-        if (PK_RARE(s.frame_done)) {
+        if (PK_RARE((s.frame_done != 0u) | (budget > 16u * FRAME_CYCLES))) {  // frame end or watchdog
             s.frame_done = 0;
             budget = 0;
             frame += 1u;
