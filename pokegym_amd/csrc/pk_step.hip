@@ -473,11 +473,17 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         const u32 addr0 = (asrc + (u32)sfield(D, PK_DB_AOFF, 2)) & 0xFFFFu;
         const u32 addr1 = (addr0 + (u32)sfield(D, PK_DB_ADIR, 2)) & 0xFFFFu;
         // image offsets of both addresses, shared by the fast read and write paths
-        const u32 o0 = fast_phys(addr0) * PK_LANES + c.lane, o1 = fast_phys(addr1) * PK_LANES + c.lane;
+        // The fast paths take a pair (addr1 = addr0 + ADIR, ADIR in -1/0/+1) only inside one
+        // 512-byte block of plain RAM, where fast_phys is linear: o1 follows from o0.  A pair that
+        // crosses a block boundary (incl. WRAM/echo at 0xE000 and echo/OAM at 0xFE00) is rare
+        // and goes through the generic bus paths.
+        const u32 o0 = fast_phys(addr0) * PK_LANES + c.lane;
+        const u32 o1 = o0 + (u32)(sfield(D, PK_DB_ADIR, 2) * (int)PK_LANES);
+        const bool fast01 = fast_ram(addr0) & fast_ram(addr1) & (((addr0 ^ addr1) & 0xFE00u) == 0u);
 
         // ---------------- memory reads (m0 at addr0, m1 at addr1) ----------------
         const bool rd = bit(D, PK_DB_RD) != 0u, rd2 = bit(D, PK_DB_RD2) != 0u;
-        const bool rram = rd & fast_ram(addr0) & fast_ram(addr1);  // addr1 == addr0 for 1-byte reads
+        const bool rram = rd & fast01;  // addr1 == addr0 for 1-byte reads
         const bool rrom = rd & rom_staged(s, addr0) & rom_staged(s, addr1);
         // each source has its own result registers, merged by OR below: sharing one register
         // would make the LDS ROM read wait for the image load of other lanes (write-after-write)
@@ -574,7 +580,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         const u32 wv = sel(bit(U, PK_UB_W16), pushv, res8);
         const bool hifirst = bit(D, PK_DB_ADIR + 1) != 0u;  // adir = -1: push writes the high byte first
         const u32 wv0 = sel(hifirst, wv >> 8, wv) & 0xFFu, wv1 = sel(hifirst, wv, wv >> 8) & 0xFFu;
-        const bool wram = wr & fast_ram(addr0) & fast_ram(addr1);
+        const bool wram = wr & fast01;
         if (wram) {
             // VRAM / OAM change while rendered lines are pending: rasterise them first (rare)
             // (lines are pending only in the rendered frame: test that first, alone)

@@ -185,3 +185,34 @@ def fuzz_source(seed: int, n_blocks: int = 160, n_banks: int = 8) -> str:
 
 def fuzz_rom(seed: int, n_blocks: int = 160, n_banks: int = 8) -> bytes:
     return build_rom(fuzz_source(seed, n_blocks, n_banks), n_banks=n_banks, title=f"FUZZ{seed}")
+
+
+def boundary_rom() -> bytes:
+    """16-bit accesses straddling the RAM region seams (WRAM/echo at 0xE000, echo/OAM at 0xFE00,
+    IO/HRAM at 0xFF80, VRAM/SRAM at 0xA000): PUSH/POP/CALL/RET with SP at the seams, LD (nn),SP
+    and LD A,[HL+]/LD [HL-],A over them, with values that change every pass (joypad-dependent)."""
+    L = ["section 0"]
+    L += ["org $0040", "reti", "org $0048", "reti", "org $0050", "reti", "org $0058", "reti", "org $0060", "reti"]
+    L += ["org $0100", "nop", "jp start", "org $0150"]
+    L += ["start:", "di", "ld sp, $dff0", "ld a, $e3", "ldh [$40], a", "ld bc, $1234", "ld de, $5678",
+          "main:",
+          # joypad bits feed the values, so each env's action stream changes them
+          "ld a, $10", "ldh [$00], a", "ldh a, [$00]", "add a, c", "ld c, a", "inc b", "inc d", "dec e",
+          # SP at the seams: PUSH writes [SP-1], [SP-2]; POP reads [SP], [SP+1]
+          "ld hl, $0000", "add hl, sp", "ld sp, $e001", "push bc", "pop de", "push de",
+          "ld sp, $fe01", "push bc", "pop hl", "push hl",
+          "ld sp, $e000", "call sub_seam",
+          "ld sp, $dfff", "pop af", "push af",
+          "ld sp, $fdff", "pop bc", "push bc",
+          # LD (nn),SP across the seams
+          "ld sp, $1357", "ld [$dfff], sp", "ld sp, $2468", "ld [$fdff], sp", "ld sp, $9abc", "ld [$9fff], sp",
+          "ld sp, $dff0",
+          # [HL+] / [HL-] walking over the seams
+          "ld hl, $dffe", "ld a, c", "ld [hl+], a", "ld [hl+], a", "ld [hl+], a",
+          "ld hl, $fdfe", "ld a, e", "ld [hl+], a", "ld [hl+], a", "ld a, [hl-]", "ld a, [hl-]", "ld c, a",
+          "ld hl, $ff7f", "ld a, [hl+]", "ld a, b", "ld [hl-], a", "ld a, [hl]",
+          "ld hl, $c000", "ld a, [$dfff]", "ld [hl+], a", "ld a, [$e000]", "ld [hl+], a",
+          "ld a, [$fdff]", "ld [hl+], a", "ld a, [$fe00]", "ld [hl+], a", "ld a, [$ff80]", "ld [hl+], a",
+          "jp main",
+          "sub_seam:", "ld a, d", "ld [$dffd], a", "ret"]
+    return build_rom("\n".join(L), n_banks=2, title="SEAMS")

@@ -47,6 +47,15 @@ def test_fuzz_rom_parity(seed):
     assert not bad, bad[:4]
 
 
+def test_region_seams_parity():
+    """16-bit accesses across the RAM region seams (K1 takes them through the generic bus)."""
+    from pokegym_amd.testrom.fuzz import boundary_rom
+    n, steps = 64, 4
+    gpu, ref = _run_both(boundary_rom(), None, n, steps, 9)
+    bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
+    assert not bad, bad[:4]
+
+
 def test_bulbasaur_state_parity():
     """Start from the reference's Bulbasaur.state (Oak's lab) under a fuzz ROM."""
     st = open(os.path.join(os.path.dirname(GOLD), "..", "pokegym_amd", "states", "Bulbasaur.state"), "rb").read()

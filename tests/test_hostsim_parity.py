@@ -25,3 +25,9 @@ def test_hostsim_game():
 
 def test_hostsim_bulbasaur_state():
     assert check(fuzz_rom(21), 4, 3, 4, state=open(STATE, "rb").read()) == []
+
+
+def test_hostsim_region_seams():
+    """16-bit accesses across the RAM region seams take the generic bus path (K1 pair rule)."""
+    from pokegym_amd.testrom.fuzz import boundary_rom
+    assert check(boundary_rom(), 8, 2, 9) == []
