@@ -479,12 +479,14 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         // and goes through the generic bus paths.
         const u32 o0 = fast_phys(addr0) * PK_LANES + c.lane;
         const u32 o1 = o0 + (u32)(sfield(D, PK_DB_ADIR, 2) * (int)PK_LANES);
-        const bool fast01 = fast_ram(addr0) & fast_ram(addr1) & (((addr0 ^ addr1) & 0xFE00u) == 0u);
+        const bool pair = ((addr0 ^ addr1) & 0xFE00u) == 0u;  // both in one 512-byte block
+        const bool fast01 = fast_ram(addr0) & fast_ram(addr1) & pair;
 
         // ---------------- memory reads (m0 at addr0, m1 at addr1) ----------------
         const bool rd = bit(D, PK_DB_RD) != 0u, rd2 = bit(D, PK_DB_RD2) != 0u;
         const bool rram = rd & fast01;  // addr1 == addr0 for 1-byte reads
-        const bool rrom = rd & rom_staged(s, addr0) & rom_staged(s, addr1);
+        // staged ROM is 16 KB-aligned: inside one block addr1 is staged iff addr0 is, at index + ADIR
+        const bool rrom = rd & rom_staged(s, addr0) & pair;
         // each source has its own result registers, merged by OR below: sharing one register
         // would make the LDS ROM read wait for the image load of other lanes (write-after-write)
         u32 rm0 = 0, rm1 = 0, om0 = 0, om1 = 0, xm = 0;
@@ -493,8 +495,9 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             if (rd2) rm1 = c.g[o1];
         }
         if (rrom) {
-            om0 = lds_rom[rom_lds_index(s, addr0)];
-            om1 = lds_rom[rom_lds_index(s, addr1)];  // == om0 for 1-byte reads, masked below
+            const u32 i0 = rom_lds_index(s, addr0);
+            om0 = lds_rom[i0];
+            om1 = lds_rom[i0 + (u32)sfield(D, PK_DB_ADIR, 2)];  // == om0 for 1-byte reads, masked below
         }
         if (PK_RARE(rd & !rram & !rrom)) {  // rare: IO registers (LY, STAT, joypad, ...), SRAM, unstaged ROM
             if (!rd2 & (addr0 >= 0xFF00u) & ((addr0 < 0xFF80u) | (addr0 == 0xFFFFu))) {
