@@ -142,10 +142,22 @@ __device__ __forceinline__ u32 slot_base(u32 bank) {
 // and the exact unfolded state is restored before anything else depends on it (STAT write, kernel
 // exit).  The event at the line end sees the same state as in the unfolded sequence except the
 // stored mode 2 instead of 0, which only feeds the mode-change interrupt test (disabled here).
-#define PK_LCD_FOLD (1u << 26)  // lcd2 bit: current line folded (next-mode field = bits 24-25)
+// Folded frame: when in addition the LY=LYC interrupt is off, a visible line's mode-2 event
+// schedules the VBlank event (line 144) directly; LY and the coincidence bit are then derived
+// from the clock too (LY/STAT read), and restored exactly on LCDC/STAT/LYC writes and at exit.
+#define PK_LCD_FOLD (1u << 26)   // lcd2 bit: current line folded (next-mode field = bits 24-25)
+#define PK_LCD_FFOLD (1u << 27)  // lcd2 bit: rest of the visible frame folded (next event: VBlank)
 __device__ __forceinline__ u32 lcd_fold_off(const St& s) { return s.clock - (s.target - 456u); }
 __device__ __forceinline__ u32 lcd_fold_mode(u32 off) { return sel(off < 80u, 2u, sel(off < 250u, 3u, 0u)); }
 __device__ __forceinline__ void lcd_unfold(St& s) {
+    if (s.lcd2 & PK_LCD_FFOLD) {  // -> the current line, folded
+        const u32 k = (s.target - s.clock - 1u) / 456u;  // whole lines left after the current one
+        const u32 ly = 143u - k, lyc = s.lcd0 >> 24;
+        const u32 stat = (bfe8(s.lcd0, 8) & 0xFBu) | sel(ly == lyc, 4u, 0u);  // its mode-2 event's LYC test
+        s.lcd0 = (s.lcd0 & 0xFF0000FFu) | (stat << 8) | (ly << 16);
+        s.target -= 456u * k;
+        s.lcd2 = (s.lcd2 & 0x00FFFFFFu) | (sel(ly < 143u, 2u, 1u) << 24) | PK_LCD_FOLD;
+    }
     if (s.lcd2 & PK_LCD_FOLD) {
         const u32 off = lcd_fold_off(s);
         s.lcd0 = (s.lcd0 & ~0x300u) | (lcd_fold_mode(off) << 8);
@@ -203,7 +215,11 @@ __device__ __forceinline__ u32 io_read(const Ctx& c, const St& s, u32 a) {
         const u32 e = (u32)(tab >> (4u * k)) & 15u;
         const u32 w = sel((e >> 2) == 0u, s.lcd0, sel((e >> 2) == 1u, s.lcd1, sel((e >> 2) == 2u, s.lcd2, 0u)));
         v = bfe8(w, 8u * (e & 3u));
-        if (k == 1u && (s.lcd2 & PK_LCD_FOLD)) v = (v & 0xFCu) | lcd_fold_mode(lcd_fold_off(s));
+        if ((k == 1u || k == 4u) && (s.lcd2 & (PK_LCD_FOLD | PK_LCD_FFOLD))) {  // STAT / LY of a folded line or frame
+            St t = s;
+            lcd_unfold(t);
+            v = bfe8(t.lcd0, sel(k == 1u, 8u, 16u));
+        }
     }
     return v;
 }
@@ -254,7 +270,10 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
             case 0xFF06: s.tim0 = setb8(s.tim0, 16, v); break;
             case 0xFF07: s.tim0 = setb8(s.tim0, 24, v & 7u); break;
             case 0xFF0F: s.cpu = setb8(s.cpu, 16, v); break;
-            case 0xFF40: lcd_set_lcdc(s, v); break;
+            case 0xFF40:
+                lcd_unfold(s);
+                lcd_set_lcdc(s, v);
+                break;
             case 0xFF41:
                 lcd_unfold(s);
                 s.lcd0 = setb8(s.lcd0, 8, (bfe8(s.lcd0, 8) & 0x87u) | (v & 0x78u));
@@ -262,7 +281,10 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
             case 0xFF42: s.lcd1 = setb8(s.lcd1, 0, v); break;
             case 0xFF43: s.lcd1 = setb8(s.lcd1, 8, v); break;
             case 0xFF44: break;  // LY is read-only
-            case 0xFF45: s.lcd0 = setb8(s.lcd0, 24, v); break;
+            case 0xFF45:
+                lcd_unfold(s);
+                s.lcd0 = setb8(s.lcd0, 24, v);
+                break;
             case 0xFF46: {  // OAM DMA: instantaneous 160-byte copy (pyboy mb.transfer_DMA)
                 if (s.npend) {
                     flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.env, c.gid);
@@ -684,7 +706,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         const bool lcdev = (lcdc & 0x80u) && s.clock >= s.target;
         if (lcdev) {  // lcd.tick mode transition
             const u32 nm = (s.lcd2 >> 24) & 3u;
-            u32 stat = bfe8(s.lcd0, 8), ly = bfe8(s.lcd0, 16);
+            u32 stat = bfe8(s.lcd0, 8), ly = sel(s.lcd2 & PK_LCD_FFOLD, 143u, bfe8(s.lcd0, 16));
             const u32 lyc = s.lcd0 >> 24;
             const bool changed = (stat & 3u) != nm;
             stat = (stat & 0xFCu) | nm;
@@ -695,16 +717,17 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             s.target -= sel(wrap && s.target >= FRAME_CYCLES, FRAME_CYCLES, 0u);
             ly = sel(wrap, 0u, sel(m2 || m1, ly + 1u, ly));
             const bool fold = m2 && (stat & 0x38u) == 0u && !s.render;  // see lcd_unfold
-            s.target += sel(fold, 456u, sel(m2, 80u, sel(m3, 170u, sel(m0, 206u, 456u))));
+            const bool ffold = fold && (stat & 0x40u) == 0u && ly < 143u;
+            s.target += sel(ffold, 456u * (144u - ly), sel(fold, 456u, sel(m2, 80u, sel(m3, 170u, sel(m0, 206u, 456u)))));
             const bool eq = lyc == ly, upd = m2 || m1;
             stat = sel(upd, sel(eq, stat | 4u, stat & 0xFBu), stat);
             irq |= sel(upd && eq && (stat & 0x40u), 2u, 0u);
-            const u32 nnext = sel(m2 && !fold, 3u, sel(m3, 0u, sel(m0 || fold, sel(ly < 143u, 2u, 1u), sel(ly == 153u, 2u, 1u))));
+            const u32 nnext = sel(m2 && !fold, 3u, sel(m3, 0u, sel(m0 || fold, sel(ly < 143u && !ffold, 2u, 1u), sel(ly == 153u, 2u, 1u))));
             const bool vbl = m1 && ly == 144u;
             irq |= sel(vbl, 1u, 0u);
             s.frame_done |= sel(vbl, 1u, 0u);
             s.lcd0 = (s.lcd0 & 0xFF0000FFu) | (stat << 8) | (ly << 16);
-            s.lcd2 = (s.lcd2 & 0x00FFFFFFu) | (nnext << 24) | sel(fold, PK_LCD_FOLD, 0u);
+            s.lcd2 = (s.lcd2 & 0x00FFFFFFu) | (nnext << 24) | sel(ffold, PK_LCD_FFOLD, sel(fold, PK_LCD_FOLD, 0u));
         }
         ev |= sel(lcdev, PK_EV_LCD, 0u);
         {
