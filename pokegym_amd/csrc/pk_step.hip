@@ -146,17 +146,20 @@ __device__ __forceinline__ u32 slot_base(u32 bank) {
 // schedules the VBlank event (line 144) directly; LY and the coincidence bit are then derived
 // from the clock too (LY/STAT read), and restored exactly on LCDC/STAT/LYC writes and at exit.
 #define PK_LCD_FOLD (1u << 26)   // lcd2 bit: current line folded (next-mode field = bits 24-25)
-#define PK_LCD_FFOLD (1u << 27)  // lcd2 bit: rest of the visible frame folded (next event: VBlank)
+#define PK_LCD_FFOLD (1u << 27)  // lcd2 bit: folded run of lines: the rest of the visible frame
+                                 // (next mode 1: VBlank event) or of VBlank (next mode 2: line 0)
 __device__ __forceinline__ u32 lcd_fold_off(const St& s) { return s.clock - (s.target - 456u); }
 __device__ __forceinline__ u32 lcd_fold_mode(u32 off) { return sel(off < 80u, 2u, sel(off < 250u, 3u, 0u)); }
 __device__ __forceinline__ void lcd_unfold(St& s) {
-    if (s.lcd2 & PK_LCD_FFOLD) {  // -> the current line, folded
+    if (s.lcd2 & PK_LCD_FFOLD) {  // -> the current line (a folded visible line, or a VBlank line)
+        const bool vis = ((s.lcd2 >> 24) & 3u) == 1u;
         const u32 k = (s.target - s.clock - 1u) / 456u;  // whole lines left after the current one
-        const u32 ly = 143u - k, lyc = s.lcd0 >> 24;
-        const u32 stat = (bfe8(s.lcd0, 8) & 0xFBu) | sel(ly == lyc, 4u, 0u);  // its mode-2 event's LYC test
+        const u32 ly = sel(vis, 143u, 153u) - k, lyc = s.lcd0 >> 24;
+        const u32 stat = (bfe8(s.lcd0, 8) & 0xFBu) | sel(ly == lyc, 4u, 0u);  // its line-start LYC test
         s.lcd0 = (s.lcd0 & 0xFF0000FFu) | (stat << 8) | (ly << 16);
         s.target -= 456u * k;
-        s.lcd2 = (s.lcd2 & 0x00FFFFFFu) | (sel(ly < 143u, 2u, 1u) << 24) | PK_LCD_FOLD;
+        const u32 nm = sel(vis, sel(ly < 143u, 2u, 1u), sel(ly == 153u, 2u, 1u));
+        s.lcd2 = (s.lcd2 & 0x00FFFFFFu) | (nm << 24) | sel(vis, PK_LCD_FOLD, 0u);
     }
     if (s.lcd2 & PK_LCD_FOLD) {
         const u32 off = lcd_fold_off(s);
@@ -662,6 +665,9 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         // Both halted-CPU blocks sit behind one `if`: a wave has a halted lane in only a few % of
         // its iterations, so the others skip their ~50 instructions.
         if (PK_RARE(s.cpu & CPU_HALT)) {
+            // a halted CPU fast-forwards to the next LCD event and notices pending interrupts only
+            // there, so folded events are observable here: restore the exact event state first
+            lcd_unfold(s);
             const u32 cpu = s.cpu, stat = bfe8(s.lcd0, 8), ly = bfe8(s.lcd0, 16), nm = (s.lcd2 >> 24) & 3u;
             const bool cand = !(cpu & CPU_QUEUED) && ((cpu >> 8) & (cpu >> 16) & 0x1Fu) == 0u
                            && (s.lcd0 & 0x80u) && (stat & 0x68u) == 0u && !(tac & 4u) && !s.render && ly < 143u && nm != 1u && s.clock <= s.target;
@@ -706,7 +712,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         const bool lcdev = (lcdc & 0x80u) && s.clock >= s.target;
         if (lcdev) {  // lcd.tick mode transition
             const u32 nm = (s.lcd2 >> 24) & 3u;
-            u32 stat = bfe8(s.lcd0, 8), ly = sel(s.lcd2 & PK_LCD_FFOLD, 143u, bfe8(s.lcd0, 16));
+            u32 stat = bfe8(s.lcd0, 8), ly = sel(s.lcd2 & PK_LCD_FFOLD, sel(nm == 1u, 143u, 153u), bfe8(s.lcd0, 16));
             const u32 lyc = s.lcd0 >> 24;
             const bool changed = (stat & 3u) != nm;
             stat = (stat & 0xFCu) | nm;
@@ -717,12 +723,15 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             s.target -= sel(wrap && s.target >= FRAME_CYCLES, FRAME_CYCLES, 0u);
             ly = sel(wrap, 0u, sel(m2 || m1, ly + 1u, ly));
             const bool fold = m2 && (stat & 0x38u) == 0u && !s.render;  // see lcd_unfold
-            const bool ffold = fold && (stat & 0x40u) == 0u && ly < 143u;
-            s.target += sel(ffold, 456u * (144u - ly), sel(fold, 456u, sel(m2, 80u, sel(m3, 170u, sel(m0, 206u, 456u)))));
+            // folded runs: the rest of the visible frame, or VBlank lines 145-153 (from the VBlank event)
+            const bool vfold = m1 && ly == 144u && (stat & 0x40u) == 0u;
+            const bool ffold = (fold && (stat & 0x40u) == 0u && ly < 143u) || vfold;
+            s.target += sel(ffold, 456u * sel(vfold, 10u, 144u - ly), sel(fold, 456u, sel(m2, 80u, sel(m3, 170u, sel(m0, 206u, 456u)))));
             const bool eq = lyc == ly, upd = m2 || m1;
             stat = sel(upd, sel(eq, stat | 4u, stat & 0xFBu), stat);
             irq |= sel(upd && eq && (stat & 0x40u), 2u, 0u);
-            const u32 nnext = sel(m2 && !fold, 3u, sel(m3, 0u, sel(m0 || fold, sel(ly < 143u && !ffold, 2u, 1u), sel(ly == 153u, 2u, 1u))));
+            const u32 nnext = sel(m2 && !fold, 3u, sel(m3, 0u, sel(m0 || fold, sel(ly < 143u && !ffold, 2u, 1u),
+                                                                   sel(ly == 153u || vfold, 2u, 1u))));
             const bool vbl = m1 && ly == 144u;
             irq |= sel(vbl, 1u, 0u);
             s.frame_done |= sel(vbl, 1u, 0u);
