@@ -14,7 +14,7 @@ STATE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
                      "Bulbasaur.state")
 
 
-@pytest.mark.parametrize("seed", [0, 1, 3, 5, 11, 21])
+@pytest.mark.parametrize("seed", [0, 1, 3, 5, 11, 21, 33, 47, 58, 71])
 def test_hostsim_fuzz(seed):
     assert check(fuzz_rom(seed), 8, 3, seed) == []
 
