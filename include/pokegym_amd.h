@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PK_ABI_VERSION 3
+#define PK_ABI_VERSION 4
 #define PK_STATE_V9_BYTES 142610u
 #define PK_SCREEN_ROWS 144u
 #define PK_SCREEN_COLS 160u
@@ -102,6 +102,12 @@ int pk_reset(pk_handle* h, const uint8_t* env_mask_dev, void* stream);
 int pk_step(pk_handle* h, const uint8_t* actions_dev, uint8_t* screen_dev, double* rew_dev,
             uint8_t* term_dev, uint8_t* trunc_dev, void* stream);
 
+/* Rasterise every env's 144 latched scanlines (the per-line SCX/SCY/WX/WY/tile-data latches that
+ * pk_create / pk_load_env restore from a v9 savestate, or that the last rendered frame latched)
+ * into the screen with K2, the HIP renderer of pk_step — PyBoy's renderer.scanline over a loaded
+ * state (the reference's 264 savestate frames pin it). Stream-ordered. */
+int pk_render_latched(pk_handle* h, void* stream);
+
 /* device pointer to the persistent u8[n][144][160] grey screen */
 uint8_t* pk_screen_ptr(pk_handle* h);
 /* device pointer to the u8[n][72][80][4] observation (PK_F_REWARD), updated by pk_step/pk_reset */
@@ -133,6 +139,9 @@ int pk_peek(pk_handle* h, uint32_t env, uint16_t addr, uint32_t len, uint8_t* ho
 int pk_poke(pk_handle* h, uint32_t env, uint16_t addr, uint32_t len, const uint8_t* host_in);
 int pk_snapshot(pk_handle* h, uint32_t env, uint8_t* host_v9, uint64_t len);
 int pk_load_env(pk_handle* h, uint32_t env, const uint8_t* host_v9, uint64_t len);
+/* v9 savestates of envs [env0, env0 + count) into host_v9 (count * PK_STATE_V9_BYTES bytes,
+ * env-major): the bulk form of pk_snapshot for whole-batch parity checks (synchronous) */
+int pk_snapshot_range(pk_handle* h, uint32_t env0, uint32_t count, uint8_t* host_v9, uint64_t len);
 
 /* Emulated instructions executed by the last pk_step, summed over envs (synchronous). */
 int pk_last_instr_count(pk_handle* h, uint64_t* out);

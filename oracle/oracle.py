@@ -178,3 +178,55 @@ def bench(rom: bytes, state: bytes | None, n: int, warmup: int, steps: int, seed
     if sec < 0:
         raise ValueError("gb_bench failed")
     return sec, int(ic.value)
+
+
+# ---------------------------------------------------------------------------------------------
+# Whole-batch parity helpers (tests only).  States are compared as 64-bit xxh3 digests of the v9
+# bytes so that 65,536-env batches fit in memory; `headless` leaves out the per-line scroll
+# parameters and the screen, which a render=False device run does not produce (the oracle always
+# renders the last frame, as pyboy_binding.py:86-87 does).
+V9_SCAN, V9_WRAM = 8405, 101285
+
+
+def state_digests(states: np.ndarray, headless: bool = False) -> np.ndarray:
+    import xxhash
+    out = np.zeros(len(states), np.uint64)
+    for i, s in enumerate(states):
+        if headless:
+            h = xxhash.xxh3_64(s[:V9_SCAN].tobytes())
+            h.update(s[V9_WRAM:].tobytes())
+            out[i] = h.intdigest()
+        else:
+            out[i] = xxhash.xxh3_64_intdigest(s.tobytes())
+    return out
+
+
+def batch_digests(rom: bytes, state, actions: np.ndarray, headless: bool = False, chunk: int = 256) -> np.ndarray:
+    """Digests of every env's v9 state after running actions (steps, n) from the template."""
+    steps, n = actions.shape
+    out = np.zeros(n, np.uint64)
+    for e0 in range(0, n, chunk):
+        st, _ = batch_run(rom, state, actions[:, e0:e0 + chunk], want_screens=False)
+        out[e0:e0 + chunk] = state_digests(st, headless)
+    return out
+
+
+def trajectory(rom: bytes, state, actions: np.ndarray, every: int, keep_every: int):
+    """Run each env of actions (steps, n) from the template; returns (digests (steps//every, n),
+    {(k, env): v9 bytes} at every keep_every steps) — checkpoints for long-horizon parity."""
+    import xxhash
+    steps, n = actions.shape
+    dig = np.zeros((steps // every, n), np.uint64)
+    keep = {}
+    for e in range(n):
+        gb = GB(rom, state)
+        if state is None:
+            gb.power_on()
+        for t in range(steps):
+            gb.run_action(int(actions[t, e]))
+            if (t + 1) % every == 0:
+                s = gb.save_state()
+                dig[(t + 1) // every - 1, e] = xxhash.xxh3_64_intdigest(s)
+                if (t + 1) % keep_every == 0:
+                    keep[((t + 1) // keep_every, e)] = s
+    return dig, keep

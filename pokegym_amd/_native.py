@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # PK_LIB selects an alternative in-tree build (A/B kernel experiments); default: lib/libpokegym_amd.so
 LIB_PATH = os.environ.get("PK_LIB") or os.path.join(HERE, "lib", "libpokegym_amd.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 PK_F_RENDER = 1
 PK_F_REWARD = 2
 PK_F_RELOAD_ON_RESET = 4
@@ -29,7 +29,8 @@ ROWS, COLS = 144, 160
 EXPORTS = ("pk_create", "pk_destroy", "pk_last_error", "pk_abi_version", "pk_reset", "pk_step",
            "pk_screen_ptr", "pk_num_envs", "pk_peek", "pk_poke", "pk_snapshot", "pk_load_env",
            "pk_last_instr_count", "pk_profile_enable", "pk_profile_read", "pk_obs_ptr", "pk_error_ptr",
-           "pk_get_ram", "pk_set_ram", "pk_info_ptr", "pk_info_flag_ptr", "pk_info_stride", "pk_heatmap_ptr", "pk_info_bits_ptr")
+           "pk_get_ram", "pk_set_ram", "pk_info_ptr", "pk_info_flag_ptr", "pk_info_stride", "pk_heatmap_ptr", "pk_info_bits_ptr",
+           "pk_snapshot_range", "pk_render_latched")
 
 
 class PkConfig(ctypes.Structure):
@@ -80,6 +81,8 @@ def load(path: str = LIB_PATH):
     L.pk_poke.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint16, ctypes.c_uint32, u8p]
     L.pk_snapshot.argtypes = [vp, ctypes.c_uint32, u8p, ctypes.c_uint64]
     L.pk_load_env.argtypes = [vp, ctypes.c_uint32, u8p, ctypes.c_uint64]
+    L.pk_snapshot_range.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u8p, ctypes.c_uint64]
+    L.pk_render_latched.argtypes = [vp, vp]
     L.pk_last_instr_count.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     L.pk_profile_enable.argtypes = [vp, ctypes.c_int]
     dp = ctypes.POINTER(ctypes.c_double)

@@ -23,7 +23,9 @@
 hipError_t pk_launch_step(const PkStepArgs& a, hipStream_t s);
 hipError_t pk_launch_render(const PkStepArgs& a, hipStream_t s);
 hipError_t pk_launch_reset(const PkResetArgs& a, hipStream_t s);
+hipError_t pk_launch_render_latched(const PkStepArgs& a, hipStream_t s);
 hipError_t pk_launch_gather_env(const uint8_t* mem, uint32_t env, uint8_t* out, hipStream_t s);
+hipError_t pk_launch_gather_range(const uint8_t* mem, uint32_t env0, uint32_t count, uint8_t* out, hipStream_t s);
 hipError_t pk_launch_scatter_env(uint8_t* mem, uint32_t env, const uint8_t* in, hipStream_t s);
 hipError_t pk_launch_done(const uint32_t* time_reg, uint32_t n, uint32_t max_steps, uint8_t* term,
                           uint8_t* trunc, double* rew, hipStream_t s);
@@ -221,6 +223,7 @@ struct pk_handle {
     uint32_t n = 0, npad = 0, ngroups = 0;
     uint32_t wave_lanes = 64;  // envs per wave in K1 (see pk_create)
     uint32_t simds = 1024;     // SIMDs of the device (4 per CU)
+    uint32_t k1_block = 0;     // K1 workgroup size override (PK_K1_BLOCK), 0 = by geometry
     uint32_t frames = 24, release = 8, flags = 0, max_steps = 20480;
     uint32_t mbc = 3, bank_mask = 0;
     uint8_t* mem = nullptr;
@@ -329,6 +332,16 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
             int v = atoi(wl);
             if (v != 64 && v != 32 && v != 16) { delete h; return fail(-EINVAL, "PK_WAVE_LANES must be 64, 32 or 16"); }
             h->wave_lanes = (uint32_t)v;
+        }
+        // K1 workgroup size override (parity tests run the benchmarked 512-thread shape at small n):
+        // a multiple of 64 whose envs fit the 256-env HRAM mirror of a workgroup
+        if (const char* bl = getenv("PK_K1_BLOCK")) {
+            int v = atoi(bl);
+            if (v < 64 || v > 512 || (v % 64) || (uint32_t)(v / 64) * h->wave_lanes > 256u) {
+                delete h;
+                return fail(-EINVAL, "PK_K1_BLOCK must be a multiple of 64 in [64, 512] with (block/64)*wave_lanes <= 256");
+            }
+            h->k1_block = (uint32_t)v;
         }
     }
     h->frames = cfg->frame_skip;
@@ -494,13 +507,9 @@ int pk_set_ram(pk_handle* h, uint16_t addr, uint32_t len, const uint8_t* dense, 
     return 0;
 }
 
-int pk_step(pk_handle* h, const uint8_t* actions, uint8_t* screen_out, double* rew, uint8_t* term,
-            uint8_t* trunc, void* stream) {
-    if (!h) return fail(-EINVAL, "null handle");
-    if (!actions) return fail(-EINVAL, "actions_dev is required");
-    HIPCHK(hipSetDevice(h->device));
-    hipStream_t s = (hipStream_t)stream;
+static PkStepArgs step_args(pk_handle* h, const uint8_t* actions) {
     PkStepArgs a;
+    memset(&a, 0, sizeof a);
     a.mem = h->mem; a.rom = h->rom; a.regs = h->regs; a.ucode = h->ucode; a.actions = actions;
     a.lat = h->lat; a.screen = h->screen; a.n = h->n; a.npad = h->npad;
     a.rom_bank_mask = h->bank_mask; a.mbc = h->mbc; a.frames = h->frames;
@@ -509,6 +518,25 @@ int pk_step(pk_handle* h, const uint8_t* actions, uint8_t* screen_out, double* r
     a.nslots = h->nslots; a.bank_slot = h->bank_slot; a.slot_bank = h->slot_bank;
     a.wave_lanes = h->wave_lanes;
     a.simds = h->simds;
+    a.block = h->k1_block;
+    return a;
+}
+
+int pk_render_latched(pk_handle* h, void* stream) {
+    if (!h) return fail(-EINVAL, "null handle");
+    HIPCHK(hipSetDevice(h->device));
+    PkStepArgs a = step_args(h, nullptr);
+    HIPCHK(pk_launch_render_latched(a, (hipStream_t)stream));
+    return 0;
+}
+
+int pk_step(pk_handle* h, const uint8_t* actions, uint8_t* screen_out, double* rew, uint8_t* term,
+            uint8_t* trunc, void* stream) {
+    if (!h) return fail(-EINVAL, "null handle");
+    if (!actions) return fail(-EINVAL, "actions_dev is required");
+    HIPCHK(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    PkStepArgs a = step_args(h, actions);
     int rc;
     if (h->prof && (rc = prof_event(h, s))) return rc;
     HIPCHK(pk_launch_step(a, s));
@@ -563,6 +591,48 @@ int pk_snapshot(pk_handle* h, uint32_t env, uint8_t* out, uint64_t len) {
     return 0;
 }
 
+int pk_snapshot_range(pk_handle* h, uint32_t env0, uint32_t count, uint8_t* out, uint64_t len) {
+    if (!h || !out) return fail(-EINVAL, "null argument");
+    if (count == 0) return 0;
+    if ((uint64_t)env0 + count > h->n) return fail(-EINVAL, "envs [%u, %u) out of range (n=%u)", env0, env0 + count, h->n);
+    if (len < (uint64_t)count * S_SIZE) return fail(-EINVAL, "buffer too small for %u v9 states", count);
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    const uint32_t chunk = count < 1024u ? count : 1024u;
+    uint8_t* dmem = nullptr;
+    HIPCHK(hipMalloc((void**)&dmem, (size_t)chunk * PK_PHYS));
+    std::vector<uint8_t> mem((size_t)chunk * PK_PHYS), screen((size_t)chunk * PK_SCREEN);
+    std::vector<uint32_t> regs((size_t)PK_NREGS * chunk), latg;
+    int rc = 0;
+    for (uint32_t c0 = 0; c0 < count && !rc; c0 += chunk) {
+        const uint32_t e0 = env0 + c0, m = (count - c0) < chunk ? (count - c0) : chunk;
+        hipError_t e = pk_launch_gather_range(h->mem, e0, m, dmem, nullptr);
+        if (e == hipSuccess) e = hipMemcpy(mem.data(), dmem, (size_t)m * PK_PHYS, hipMemcpyDeviceToHost);
+        for (uint32_t f = 0; f < PK_NREGS && e == hipSuccess; f++)
+            e = hipMemcpy(&regs[(size_t)f * chunk], h->regs + (size_t)f * h->npad + e0, (size_t)m * 4, hipMemcpyDeviceToHost);
+        if (e == hipSuccess)
+            e = hipMemcpy(screen.data(), h->screen + (size_t)e0 * PK_SCREEN, (size_t)m * PK_SCREEN, hipMemcpyDeviceToHost);
+        // latches of the groups covering [e0, e0 + m)
+        const uint32_t g0 = e0 / PK_LANES, g1 = (e0 + m - 1) / PK_LANES + 1, rows = (g1 - g0) * PK_ROWS * PK_LANES;
+        latg.resize((size_t)3 * rows);
+        for (uint32_t k = 0; k < 3 && e == hipSuccess; k++)
+            e = hipMemcpy(&latg[(size_t)k * rows], h->lat + k * h->lat_stride + (size_t)g0 * PK_ROWS * PK_LANES,
+                          (size_t)rows * 4, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) { rc = fail(-EIO, "pk_snapshot_range: %s", hipGetErrorString(e)); break; }
+        for (uint32_t i = 0; i < m; i++) {
+            const uint32_t env = e0 + i, gi = env / PK_LANES - g0, lane = env % PK_LANES;
+            uint32_t r[PK_NREGS], lat[3 * PK_ROWS];
+            for (uint32_t f = 0; f < PK_NREGS; f++) r[f] = regs[(size_t)f * chunk + i];
+            for (uint32_t k = 0; k < 3; k++)
+                for (uint32_t y = 0; y < PK_ROWS; y++)
+                    lat[k * PK_ROWS + y] = latg[(size_t)k * rows + ((size_t)gi * PK_ROWS + y) * PK_LANES + lane];
+            export_v9(h->tmpl, r, &mem[(size_t)i * PK_PHYS], lat, &screen[(size_t)i * PK_SCREEN], out + (size_t)(c0 + i) * S_SIZE);
+        }
+    }
+    (void)hipFree(dmem);
+    return rc;
+}
+
 int pk_load_env(pk_handle* h, uint32_t env, const uint8_t* in, uint64_t len) {
     if (!h || !in) return fail(-EINVAL, "null argument");
     if (env >= h->n) return fail(-EINVAL, "env %u out of range", env);
@@ -574,7 +644,10 @@ int pk_load_env(pk_handle* h, uint32_t env, const uint8_t* in, uint64_t len) {
     HIPCHK(hipMemcpy(h->scratch, t.mem.data(), PK_PHYS, hipMemcpyHostToDevice));
     HIPCHK(pk_launch_scatter_env(h->mem, env, h->scratch, nullptr));
     HIPCHK(hipDeviceSynchronize());
-    for (uint32_t f = 0; f < PK_NREGS; f++)
+    // machine state only: the env's step counter (PK_R_TIME, pokegym `self.time`) and the per-step
+    // bookkeeping slots survive a load, as in load_pyboy_state (pyboy_binding.py:59-62), which
+    // leaves self.time alone; only reset() zeroes it
+    for (uint32_t f = 0; f <= PK_R_MISC; f++)
         HIPCHK(hipMemcpy(h->regs + (size_t)f * h->npad + env, &t.regs[f], 4, hipMemcpyHostToDevice));
     uint32_t gid = env / PK_LANES, lane = env % PK_LANES;
     for (uint32_t k = 0; k < 3; k++)

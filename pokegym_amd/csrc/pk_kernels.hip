@@ -41,6 +41,24 @@ __global__ void __launch_bounds__(64) pk_render_kernel(PkStepArgs A) {
     A.lat[2u * A.lat_stride + idx] = l2 & ~0x100u;
 }
 
+// Re-arm every env's 144 latched lines for K2 (pk_render_latched): the window line counter of each
+// line follows from the latched LCDC/WY/WX as K1 derives it at latch time (pyboy renderer: the
+// window counter advances on lines where the window is enabled, started and on screen).
+__global__ void __launch_bounds__(256) pk_arm_latches_kernel(PkStepArgs A) {
+    const u32 env = blockIdx.x * blockDim.x + threadIdx.x;
+    if (env >= A.n) return;
+    const u32 gid = env / PK_LANES, lane = env % PK_LANES;
+    int lw = -1;
+    for (u32 y = 0; y < PK_ROWS; y++) {
+        const u32 idx = (gid * PK_ROWS + y) * PK_LANES + lane;
+        const u32 l0 = A.lat[idx], l1 = A.lat[A.lat_stride + idx];
+        const u32 wy = l1 & 0xFFu, wx = bfe8(l0, 24);
+        if ((l0 & 0x20u) && wy <= y && (int)wx - 7 < (int)PK_COLS) lw += 1;
+        A.lat[2u * A.lat_stride + idx] = (u32)(lw + 1) | 0x100u;
+    }
+    A.regs[PK_R_RFLAGS * A.npad + env] &= ~1u;
+}
+
 // ---------------------------------------------------------------------------------------------
 // K5: reset selected envs from the template (regs + RAM image + screen + line latches).
 
@@ -86,6 +104,17 @@ __global__ void pk_gather_env_kernel(const u8* mem, u32 env, u8* out) {
         out[p] = g[p * PK_LANES + lane];
 }
 
+// gather envs [env0, env0 + count) into out[count][PK_PHYS] (bulk snapshots): one thread per
+// (phys row, env) with env fastest, so each wave reads 64 consecutive interleaved bytes
+__global__ void __launch_bounds__(256) pk_gather_range_kernel(const u8* mem, u32 env0, u32 count, u8* out) {
+    const size_t total = (size_t)count * PK_PHYS;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+        const u32 k = (u32)(t % count), p = (u32)(t / count);
+        const u32 env = env0 + k;
+        out[(size_t)k * PK_PHYS + p] = mem[(size_t)(env / PK_LANES) * PK_GROUP_STRIDE + (size_t)p * PK_LANES + env % PK_LANES];
+    }
+}
+
 __global__ void pk_scatter_env_kernel(u8* mem, u32 env, const u8* in) {
     const u32 gid = env / PK_LANES, lane = env % PK_LANES;
     u8* g = mem + (size_t)gid * PK_GROUP_STRIDE;
@@ -101,6 +130,13 @@ hipError_t pk_launch_render(const PkStepArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+hipError_t pk_launch_render_latched(const PkStepArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(pk_arm_latches_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return pk_launch_render(a, s);
+}
+
 hipError_t pk_launch_reset(const PkResetArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(pk_reset_mem_kernel, dim3(2048), dim3(256), 0, s, a);
     hipError_t e = hipGetLastError();
@@ -111,6 +147,11 @@ hipError_t pk_launch_reset(const PkResetArgs& a, hipStream_t s) {
 
 hipError_t pk_launch_gather_env(const u8* mem, u32 env, u8* out, hipStream_t s) {
     hipLaunchKernelGGL(pk_gather_env_kernel, dim3(64), dim3(256), 0, s, mem, env, out);
+    return hipGetLastError();
+}
+
+hipError_t pk_launch_gather_range(const u8* mem, u32 env0, u32 count, u8* out, hipStream_t s) {
+    hipLaunchKernelGGL(pk_gather_range_kernel, dim3(2048), dim3(256), 0, s, mem, env0, count, out);
     return hipGetLastError();
 }
 

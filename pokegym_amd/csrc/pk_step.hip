@@ -805,7 +805,7 @@ hipError_t pk_launch_step(const PkStepArgs& a, hipStream_t s) {
     const u32 wl = a.wave_lanes;
     const u32 threads = a.npad * (PK_LANES / wl);
     const u32 wide = 256u * PK_LANES / wl < PK_K1_MAX_THREADS ? 256u * PK_LANES / wl : PK_K1_MAX_THREADS;
-    const u32 block = threads / PK_LANES <= a.simds ? 256u : wide;
+    const u32 block = a.block ? a.block : (threads / PK_LANES <= a.simds ? 256u : wide);
     const u32 grid = (threads + block - 1) / block;
     hipLaunchKernelGGL(pk_step_kernel, dim3(grid), dim3(block), 0, s, a);
     return hipGetLastError();

@@ -53,11 +53,15 @@ class EpisodeStats:
         self.ep_return.mul_(keep)
         self.ep_length.mul_(keep)
 
-    def allreduce(self, group=None) -> dict:
-        """Sum the summaries of all ranks (RCCL over xGMI when the tensors live on GPUs)."""
+    def allreduce(self, group=None, reset: bool = True) -> dict:
+        """Sum the summaries of all ranks (RCCL over xGMI when the tensors live on GPUs).  With
+        reset (the default, like InfoStats) the summary restarts, so each call covers one logging
+        interval; per-env episodes in progress keep accumulating."""
         out = self.summary.clone()
         if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
             dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
+        if reset:
+            self.summary.zero_()
         vals = out.tolist()
         res = dict(zip(STAT_FIELDS, vals))
         res["mean_episodic_return"] = vals[0] / vals[1] if vals[1] else float("nan")

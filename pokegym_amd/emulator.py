@@ -165,6 +165,18 @@ class BatchedEmulator:
               "pk_snapshot")
         return out.tobytes()
 
+    def snapshot_range(self, env0: int, count: int) -> np.ndarray:
+        """v9 savestates of envs [env0, env0 + count) as a (count, 142610) uint8 array (bulk pk_snapshot)."""
+        out = np.zeros((count, STATE_V9_BYTES), np.uint8)
+        check(self._L.pk_snapshot_range(self._h, env0, count, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                        out.size), "pk_snapshot_range")
+        return out
+
+    def render_latched(self):
+        """Rasterise every env's latched scanlines into `screen` (K2 over a loaded state)."""
+        check(self._L.pk_render_latched(self._h, self._stream()), "pk_render_latched")
+        return self.screen
+
     def load_env(self, env: int, state: bytes):
         a, p = _u8p(state)
         check(self._L.pk_load_env(self._h, env, p, len(a)), "pk_load_env")

@@ -133,11 +133,31 @@ class VecEnv:
         self.log_interval = log_interval
         self.t = 0
         self._pending = None
+        # first PK_ERR_* code of every env since the last check: the device clears an env's error
+        # word when the env auto-resets, so the codes are kept here (no host sync) and raised at
+        # the next logging interval — an exception between two checks is not lost
+        errs = getattr(emulator, "errors", None)
+        self.sticky_errors = torch.zeros_like(errs) if errs is not None else None
 
     def reset(self, seed=None):
         obs = self.emu.reset()
         self.t = 0
+        if self.sticky_errors is not None:
+            self.sticky_errors.zero_()
         return obs, []
+
+    def raise_if_failed(self):
+        """Raise the reference's exception for the first env that hit one since the last check."""
+        if self.sticky_errors is None:
+            return
+        bad = torch.nonzero(self.sticky_errors).flatten()
+        if bad.numel():
+            from ._native import ERR_EXCEPTIONS
+            e = int(bad[0])
+            code = int(self.sticky_errors[e])
+            self.sticky_errors.zero_()
+            raise ERR_EXCEPTIONS.get(code, RuntimeError)(
+                f"env {e}: reference reward stack raises here (PK_ERR {code}); {bad.numel()} env(s) failed")
 
     def step(self, actions):
         if isinstance(actions, np.ndarray):
@@ -150,12 +170,13 @@ class VecEnv:
         self.stats.update(rewards, term)
         if self.info_stats is not None:
             self.info_stats.update(self.emu.info, self.emu.info_flag)
+        if self.sticky_errors is not None:
+            torch.where(self.sticky_errors != 0, self.sticky_errors, self.emu.errors, out=self.sticky_errors)
         self.emu.reset(term)  # auto-reset finished envs (no host sync)
         self.t += 1
         infos = []
         if self.log_interval and self.t % self.log_interval == 0:
-            if hasattr(self.emu, "raise_if_failed"):
-                self.emu.raise_if_failed()
+            self.raise_if_failed()
             infos = [self.stats.allreduce()]
             if self.info_stats is not None:
                 infos[0].update(self.info_stats.allreduce())

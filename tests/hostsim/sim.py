@@ -30,6 +30,8 @@ def lib():
         L.pk_load_env.argtypes = [vp, ctypes.c_uint32, u8p, ctypes.c_uint64]
         L.pk_screen_ptr.argtypes = [vp]
         L.pk_screen_ptr.restype = vp
+        L.pk_snapshot_range.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u8p, ctypes.c_uint64]
+        L.pk_render_latched.argtypes = [vp, vp]
         _lib = L
     return _lib
 
@@ -63,6 +65,24 @@ class SimEmulator:
         out = np.zeros(142610, np.uint8)
         lib().pk_snapshot(self.h, e, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), len(out))
         return out.tobytes()
+
+    def snapshot_range(self, e0: int, count: int) -> np.ndarray:
+        out = np.zeros((count, 142610), np.uint8)
+        rc = lib().pk_snapshot_range(self.h, e0, count, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), out.size)
+        if rc:
+            raise RuntimeError(lib().pk_last_error().decode())
+        return out
+
+    def load_env(self, e: int, state: bytes):
+        a = np.frombuffer(state, np.uint8).copy()
+        rc = lib().pk_load_env(self.h, e, a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), len(a))
+        if rc:
+            raise RuntimeError(lib().pk_last_error().decode())
+
+    def render_latched(self):
+        rc = lib().pk_render_latched(self.h, None)
+        if rc:
+            raise RuntimeError(lib().pk_last_error().decode())
 
     def screen(self) -> np.ndarray:
         p = lib().pk_screen_ptr(self.h)

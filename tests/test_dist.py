@@ -40,6 +40,11 @@ def test_episode_stats_accumulate():
     assert s["episode_length_sum"] == 2 + 3 + 3
     assert s["steps"] == 9 and s["reward_sum"] == 18.0
     assert st.ep_return.tolist() == [1.0, 0.0, 0.0]
+    # the summary covers one logging interval; the open episode keeps its running return
+    st.update(r, torch.tensor([1, 0, 0], dtype=torch.uint8))
+    s = st.allreduce()
+    assert s["episodes"] == 1 and s["episodic_return_sum"] == 2.0 and s["steps"] == 3
+    assert st.allreduce(reset=False)["episodes"] == 0
 
 
 def _free_port():

@@ -60,3 +60,25 @@ def test_environment_savestates_round_trip(tmp_path):
     assert env.emu.snapshot(0) == saved
     assert len(env.load_first_state().getvalue()) == len(saved)
     env.close()
+
+
+@pytest.mark.gpu
+def test_load_state_mid_episode_keeps_step_counter():
+    """load_pyboy_state leaves self.time alone (pyboy_binding.py:59-62): done fires at the same
+    step with or without a state load in the middle of the episode."""
+    from pokegym_amd.env import Environment
+    from pokegym_amd.testrom.game import game_rom
+    done_at = []
+    for load in (False, True):
+        env = Environment(rom_path=game_rom(), max_episode_steps=5)
+        env.reset()
+        first = env.load_first_state()
+        for t in range(1, 8):
+            if load and t == 3:
+                env.load_pyboy_state(first)
+            done = env.step(0)[2]
+            if done:
+                done_at.append(t)
+                break
+        env.close()
+    assert done_at == [5, 5]

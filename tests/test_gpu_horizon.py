@@ -1,0 +1,78 @@
+"""Long-horizon parity: the HIP emulator vs the oracle over 10,000 scripted env-steps.
+
+BASELINE.json's north_star asks for bit-exact WRAM over 10k scripted steps, and the reference's
+only benchmark is 10,000 x step(0) (/root/reference/test.py:16-29).  Timing bugs (DIV-mixing RNG,
+folded LCD events, HALT skip-ahead) grow with the horizon, so this compares the WHOLE machine
+state (v9 savestate digest: WRAM, VRAM, OAM, HRAM, IO, CPU/LCD/timer/MBC registers, clocks, the
+rendered screen) every 250 env-steps along 64 trajectories of 10,000 steps each from power-on:
+trajectory 0 presses Down every step (test.py's a_t = 0), trajectory 1 the [0,3,1,2] cycle of
+configs[1], trajectories 2..63 seeded random presses 0..8 (8 = no button).
+
+The 10,000 steps of a trajectory are split into 8 segments of 1,250 that run side by side in one
+512-env launch: segment k starts from the oracle's own v9 state at step 1,250k (pk_load_env) —
+so the device is checked continuously over every step of the 10k horizon while the wall time is
+that of 1,250 steps (a single 24-frame env-step is latency-bound at ~65 ms however few envs run).
+Segment 0 starts from power-on on both sides.  tools/horizon_continuous.py runs the same
+trajectories as ONE continuous 10k-step device run (profiles/r02_horizon_continuous.log)."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+from tests import oracle_pool as OP
+
+pytestmark = pytest.mark.gpu
+
+TOTAL, SEGS, EVERY, NTRAJ = 10000, 8, 250, 64
+SEG = TOTAL // SEGS
+PARTS = SEG // EVERY
+
+
+def horizon_actions(total=TOTAL, ntraj=NTRAJ) -> np.ndarray:
+    a = np.random.default_rng(10000).integers(0, 9, (total, ntraj), dtype=np.uint8)
+    a[:, 0] = 0
+    a[:, 1] = np.array([0, 3, 1, 2], np.uint8)[np.arange(total) % 4]
+    return a
+
+
+@pytest.fixture(scope="module")
+def horizon():
+    import torch
+    from pokegym_amd.emulator import BatchedEmulator
+    from pokegym_amd.testrom.game import game_rom
+    rom = game_rom()
+    actions = horizon_actions()
+    with OP.pool() as ex:
+        dig, keep = OP.trajectories(ex, rom, None, actions, every=EVERY, keep_every=SEG, chunk=4)
+    emu = BatchedEmulator(rom, SEGS * NTRAJ, render=True)
+    for k in range(1, SEGS):
+        for j in range(NTRAJ):
+            emu.load_env(k * NTRAJ + j, keep[(k, j)])
+    # device action table: env k*64+j at local step t plays actions[k*SEG + t, j]
+    table = np.concatenate([actions[k * SEG:(k + 1) * SEG] for k in range(SEGS)], axis=1)
+    st = {"emu": emu, "acts": torch.from_numpy(np.ascontiguousarray(table)).to(emu.device), "dig": dig, "t": 0,
+          "ok": True}
+    yield st
+    emu.close()
+
+
+@pytest.mark.parametrize("part", range(PARTS))
+def test_horizon_10k_segments(horizon, part):
+    import torch
+    st = horizon
+    if not st["ok"] or st["t"] != part * EVERY:
+        pytest.skip("an earlier part of the horizon failed")
+    emu, acts = st["emu"], st["acts"]
+    st["ok"] = False
+    for t in range(part * EVERY, (part + 1) * EVERY):
+        emu.step(acts[t])
+    torch.cuda.synchronize()
+    st["t"] = (part + 1) * EVERY
+    got = oracle.state_digests(emu.snapshot_range(0, emu.n)).reshape(SEGS, NTRAJ)
+    bad = []
+    for k in range(SEGS):
+        step = k * SEG + (part + 1) * EVERY               # global env-step of this checkpoint
+        want = st["dig"][step // EVERY - 1]
+        for j in np.nonzero(got[k] != want)[0]:
+            bad.append((int(step), int(j)))
+    assert not bad, f"{len(bad)} (step, trajectory) checkpoints differ: {bad[:8]}"
+    st["ok"] = True

@@ -91,3 +91,21 @@ def test_game_rom_parity_wave_shapes(lanes, monkeypatch):
     gpu, ref = _run_both(rom, None, n, steps, 7)
     bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
     assert not bad, bad[:4]
+
+
+@pytest.mark.parametrize("seed", [-1, 0, 3, 21, 47])
+@pytest.mark.parametrize("render", [True, False])
+def test_fuzz_rom_parity_512_thread_workgroups(seed, render, monkeypatch):
+    """The benchmarked K1 shape at small n: 512-thread workgroups (PK_K1_BLOCK), 32 envs per wave,
+    8 waves sharing the workgroup's HRAM mirror (columns up to 255); rendered and headless."""
+    monkeypatch.setenv("PK_K1_BLOCK", "512")
+    monkeypatch.setenv("PK_WAVE_LANES", "32")
+    from pokegym_amd.testrom.game import game_rom
+    rom = game_rom() if seed < 0 else fuzz_rom(seed)
+    n, steps = 256, 8
+    gpu, ref = _run_both(rom, None, n, steps, 100 + seed, render=render)
+    g = np.frombuffer(b"".join(gpu), np.uint8).reshape(n, -1)
+    a = oracle.state_digests(g, headless=not render)
+    b = oracle.state_digests(ref, headless=not render)
+    bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in np.nonzero(a != b)[0][:4]]
+    assert not bad, bad

@@ -1,0 +1,131 @@
+"""HIP path vs the CPU oracle at the geometries the benchmark and BASELINE.json's configs run.
+
+The small parity tests (test_gpu_parity.py) run <= 128 envs, where K1 launches 256-thread
+workgroups.  These run the real shapes: configs[2] at its full 65,536 envs (512-thread
+workgroups, two 32-env waves per SIMD, the 256-env HRAM mirror of a workgroup fully used),
+configs[1] at 4,096 envs headless with the fixed [0,3,1,2] action cycle, and a configs[4] per-GPU
+shard (32,768 envs) with the reward stack and a template reload on every done.  Every env is
+compared: machine states as 64-bit digests of the v9 savestate (oracle.state_digests), rewards
+as exact float64, observations and WRAM as digests.  The oracle runs in spawned worker processes
+(tests/oracle_pool.py) while the GPU steps."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+from tests import oracle_pool as OP
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def gpu_digests(emu, headless=False, chunk=2048):
+    out = np.zeros(emu.n, np.uint64)
+    for e0 in range(0, emu.n, chunk):
+        st = emu.snapshot_range(e0, min(chunk, emu.n - e0))
+        out[e0:e0 + len(st)] = oracle.state_digests(st, headless)
+    return out
+
+
+def _explain(rom, state, actions, emu, env):
+    """First differing v9 offsets of one env (diagnostics for a failing digest)."""
+    ref, _ = oracle.batch_run(rom, state, np.ascontiguousarray(actions[:, env:env + 1]), want_screens=False)
+    a = emu.snapshot_range(env, 1)[0]
+    idx = np.nonzero(a != ref[0])[0]
+    return env, idx[:10].tolist()
+
+
+def _check_states(rom, state, actions, emu, futs, headless):
+    want = OP.gather_digests(futs, emu.n)
+    got = gpu_digests(emu, headless)
+    bad = np.nonzero(want != got)[0]
+    if len(bad):
+        pytest.fail(f"{len(bad)}/{emu.n} envs differ; first: {[_explain(rom, state, actions, emu, int(e)) for e in bad[:3]]}")
+
+
+def test_config3_geometry_65536_envs():
+    """configs[2]: 65,536 envs, rendered frame 24, random actions — the benchmarked launch."""
+    import torch
+    from pokegym_amd.emulator import BatchedEmulator
+    from pokegym_amd.testrom.game import game_rom
+    rom, n, steps = game_rom(), 65536, 2
+    actions = np.random.default_rng(65536).integers(0, 8, (steps, n), dtype=np.uint8)
+    with OP.pool() as ex:
+        futs = OP.batch_digests(ex, rom, None, actions, chunk=1024)
+        emu = BatchedEmulator(rom, n, render=True)
+        acts = torch.from_numpy(actions).to(emu.device)
+        for t in range(steps):
+            emu.step(acts[t])
+        torch.cuda.synchronize()
+        _check_states(rom, None, actions, emu, futs, headless=False)
+        emu.close()
+
+
+def test_config2_geometry_4096_envs_headless_cycle():
+    """configs[1]: 4,096 envs, no PPU render (LCD folding + HALT skip-ahead paths), the fixed
+    [0,3,1,2] cycle (half the envs at a per-env phase, half with random presses incl. none)."""
+    import torch
+    from pokegym_amd.emulator import BatchedEmulator
+    from pokegym_amd.testrom.game import game_rom
+    rom, n, steps = game_rom(), 4096, 8
+    cyc = np.array([0, 3, 1, 2], np.uint8)
+    actions = cyc[(np.arange(steps)[:, None] + np.arange(n)[None, :]) % 4].astype(np.uint8)
+    actions[:, n // 2:] = np.random.default_rng(4096).integers(0, 9, (steps, n // 2), dtype=np.uint8)
+    with OP.pool() as ex:
+        futs = OP.batch_digests(ex, rom, None, actions, headless=True, chunk=128)
+        emu = BatchedEmulator(rom, n, render=False)
+        acts = torch.from_numpy(actions).to(emu.device)
+        for t in range(steps):
+            emu.step(acts[t])
+        torch.cuda.synchronize()
+        _check_states(rom, None, actions, emu, futs, headless=True)
+        emu.close()
+
+
+def test_config5_shard_32768_envs_reward_reload():
+    """configs[4] per-GPU shard: 32,768 envs from Bulbasaur.state with the full reward stack, the
+    (72,80,4) obs and a template reload on EVERY done (max_episode_steps 3, so two resets fire
+    inside the run).  Every env: exact f64 rewards, dones, error codes, obs and WRAM digests."""
+    import torch
+    import xxhash
+    from pokegym_amd.emulator import BatchedEmulator
+    from pokegym_amd.testrom.game import game_rom
+    rom = game_rom()
+    state = open(os.path.join(REPO, "pokegym_amd", "states", "Bulbasaur.state"), "rb").read()
+    n, steps, max_steps = 32768, 7, 3
+    actions = np.random.default_rng(32768).integers(0, 8, (steps, n), dtype=np.uint8)
+
+    def dig(rows):
+        return np.array([xxhash.xxh3_64_intdigest(r.tobytes()) for r in rows], np.uint64)
+
+    with OP.pool() as ex:
+        parts = OP.reward_runs_async(ex, rom, state, actions, max_steps, chunk=256)
+        emu = BatchedEmulator(rom, n, state=state, render=True, reward=True, reload_on_reset=True,
+                              max_episode_steps=max_steps)
+        got_obs = np.zeros((steps + 1, n), np.uint64)
+        got_wram = np.zeros((steps, n), np.uint64)
+        got_rew = np.zeros((steps, n), np.float64)
+        got_done = np.zeros((steps, n), np.uint8)
+        got_err = np.zeros((steps, n), np.uint32)
+        got_obs[0] = dig(emu.reset().cpu().numpy())
+        acts = torch.from_numpy(actions).to(emu.device)
+        for t in range(steps):
+            obs, rew, term, trunc = emu.step(acts[t])
+            got_rew[t] = rew.cpu().numpy()
+            got_done[t] = term.cpu().numpy()
+            got_err[t] = emu.errors.cpu().numpy()
+            got_wram[t] = dig(emu.get_ram(0xC000, 8192).cpu().numpy())
+            obs = emu.reset(term)
+            got_obs[t + 1] = dig(obs.cpu().numpy())
+        emu.close()
+        rew, done, err, obs_d, wram_d = OP.gather_reward_runs(parts, steps, n)
+    live = np.cumsum(err != 0, axis=0) == 0          # an env stops being compared after its error step
+    assert np.array_equal(got_err[err != 0], err[err != 0])
+    assert (got_done[live] == done[live]).all() and done[:, :].sum() > 0
+    assert np.array_equal(got_rew[live], rew[live]), np.nonzero(got_rew != rew)
+    assert (got_wram[live] == wram_d[live]).all()
+    live_obs = np.vstack([np.ones((1, n), bool), live])
+    assert (got_obs[live_obs] == obs_d[live_obs]).all()
+    # resets fired where the reference's done did: time >= 3 after steps 3 and 6
+    assert (done[2][live[2]] == 1).all() and (done[5][live[5]] == 1).all()

@@ -55,3 +55,35 @@ def test_vecenv_async_api():
     o, r, d, t, i, ids, m = env.recv()
     assert r.tolist() == [5.0, 6.0]
     assert env.single_observation_space.shape == (72, 80, 4) and env.single_action_space.n == 8
+
+
+class FakeEmuErr(FakeEmu):
+    """env 1 hits a reference exception at step 2 and finishes (auto-reset clears its error word)."""
+
+    def __init__(self, n):
+        super().__init__(n, done_every=2)
+        self.errors = torch.zeros(n, dtype=torch.int32)
+
+    def reset(self, mask=None):
+        m = torch.ones(self.n, dtype=torch.bool) if mask is None else mask.to(torch.bool)
+        self.errors[m] = 0
+        return super().reset(mask)
+
+    def step(self, a):
+        out = super().step(a)
+        if int(self.time[1]) == 2:
+            self.errors[1] = 1   # PK_ERR_MAP_KEY -> KeyError
+        return out
+
+
+def test_vecenv_error_survives_autoreset():
+    import pytest
+    emu = FakeEmuErr(3)
+    env = VecEnv(3, emulator=emu, log_interval=4)
+    env.reset()
+    env.step(torch.zeros(3, dtype=torch.uint8))
+    env.step(torch.zeros(3, dtype=torch.uint8))     # error + done: the env is reset, its error word cleared
+    assert int(emu.errors[1]) == 0 and int(env.sticky_errors[1]) == 1
+    env.step(torch.zeros(3, dtype=torch.uint8))
+    with pytest.raises(KeyError):
+        env.step(torch.zeros(3, dtype=torch.uint8))   # raised at the logging interval
