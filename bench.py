@@ -1,15 +1,22 @@
 """Benchmark: aggregate env.step/s of the batched Pokémon Red emulator on 1..8 MI355X.
 
 Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N>1 the driver launches it
-under torch.distributed.run, one rank per GPU.  Each rank owns `--envs` emulators (weak scaling),
-does W untimed env-steps, then times exactly K env-steps between barrier+synchronize fences; the
-max elapsed over ranks gives `value` = (N * envs * K) / max_elapsed.  Rank 0 prints ONE JSON line.
+under torch.distributed.run, one rank per GPU.  Each rank owns its shard of envs, does W untimed
+env-steps, then times exactly K env-steps between barrier+synchronize fences; the max elapsed over
+ranks gives `value` = (all ranks' envs * K) / max_elapsed.  Rank 0 prints ONE JSON line.
 
-Workload (BASELINE.json configs[2], per GPU): 65,536 envs, the last of the 24 frames of every
-env-step PPU-rendered into a 160x144 u8 screen obs, actions uniform in [0,8) from a counter-based
-(Philox) RNG.  The ROM is the synthetic game `pkbench` (pokegym_amd/testrom/game.py) because
-pokemon_red.gb is not shipped; pass `--rom path --state path` to run a real cartridge.
-Inputs are resident in HBM before the timed region (actions pre-generated on device).
+Workloads (BASELINE.json configs):
+  config3 (default at N=1) configs[2]: 65,536 envs/GPU, the last of the 24 frames of every env-step
+          PPU-rendered into a 160x144 u8 screen obs, actions uniform in [0,8) (torch Philox).
+  config4 (default at N>1) configs[3]: 32,768 envs per GPU (262,144 on 8), screen obs, stepped
+          through the PufferLib-shaped VecEnv (send/recv, auto-reset); weak scaling.
+  config5 configs[4]: config4's shard + the full ram_map reward stack, the (72,80,4) obs, a template
+          reload on every done (short episodes, --max-episode-steps, so resets happen in the timed
+          steps) and the RCCL all-reduce of episode statistics every 128 steps.
+  config2 configs[1]: 4,096 envs on 1 GPU, headless (no PPU), the fixed [0,3,1,2] action cycle.
+The ROM is the synthetic game `pkbench` (pokegym_amd/testrom/game.py; --rom-banks 64 for the
+Pokémon-Red-sized 1 MiB variant) because pokemon_red.gb is not shipped; --rom/--state run a real
+cartridge.  Inputs are resident in HBM before the timed region (actions pre-generated on device).
 """
 from __future__ import annotations
 
@@ -24,10 +31,23 @@ sys.path.insert(0, HERE)
 
 # algorithmic bytes per env-step: S = 16,844 B hot state
 S_HOT = 8192 + 8192 + 160 + 127 + 128 + 1 + 44
-B_HEADLESS = 2 * S_HOT + 1 + 8 + 2          # 33,699: K1 reads+writes the hot state, action, reward, flags
-B_SCREEN = B_HEADLESS + 160 * 144           # 56,739: + the u8 screen obs (K2)
-B_REWARD = B_SCREEN + 2 * 256               # 57,251: + per-env reward accumulators (config 5)
+B_HEADLESS = 2 * S_HOT + 1 + 8 + 2          # B2 = 33,699: the hot state read+written, action, reward, flags
+B_SCREEN = B_HEADLESS + 160 * 144           # B3,4 = 56,739: + the u8 screen obs (K2)
+B_REWARD = B_SCREEN + 2 * 256               # B5 = 57,251: + per-env reward accumulators
 HBM_PEAK_GBS = 8000.0                       # MI355X_MICROARCH.md: 8.0 TB/s HBM3E
+
+WORKLOADS = {
+    "config2": dict(envs=4096, render=False, reward=False, vecenv=False, actions="cycle", bytes=B_HEADLESS,
+                    desc="configs[1]: headless (no PPU), RAM-only obs, fixed action cycle [0,3,1,2]"),
+    "config3": dict(envs=65536, render=True, reward=False, vecenv=False, actions="random", bytes=B_SCREEN,
+                    desc="configs[2]: PPU-rendered 160x144 u8 screen obs, random actions"),
+    "config4": dict(envs=32768, render=True, reward=False, vecenv=True, actions="random", bytes=B_SCREEN,
+                    desc="configs[3] shard: 32,768 envs/GPU (262,144 on 8), screen obs, PufferLib-shaped "
+                         "VecEnv send/recv with auto-reset, random actions"),
+    "config5": dict(envs=32768, render=True, reward=True, vecenv=False, actions="random", bytes=B_REWARD,
+                    desc="configs[4] shard: 32,768 envs/GPU + full ram_map reward stack + (72,80,4) obs + per-env "
+                         "template reload on done + episodic-return all-reduce every 128 steps"),
+}
 
 
 def _cpu_baseline(rom: bytes, state, seconds_target: float = 12.0):
@@ -48,16 +68,36 @@ def _cpu_baseline(rom: bytes, state, seconds_target: float = 12.0):
         wall = time.time() - t0
     total_steps = workers * n_per * steps
     slowest = max(r[0] for r in res)
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     return {
         "value": round(total_steps / slowest, 1),
         "unit": "env-steps/s",
         "cores": workers,
+        "host_cpus": os.cpu_count(),
+        "affinity_cpus": affinity,
         "kind": "port",
-        "sample": (f"{workers} processes x {n_per} envs x {steps} timed env-steps (after 3 warmup) of the same "
-                   f"ROM/workload on the C oracle (oracle/gbcore.c, 1 thread/process); aggregate over the slowest "
+        "sample": (f"{workers} worker processes (the box's CPU share; os.cpu_count() = {os.cpu_count()} is the whole "
+                   f"machine) x {n_per} envs x {steps} timed env-steps (after 3 warmup) of the same ROM on the C "
+                   f"oracle (oracle/gbcore.c, 1 thread/process, random actions); aggregate over the slowest "
                    f"process's timed span; pool wall {wall:.1f}s; PyBoy+pokegym itself is not installed"),
         "instr_per_s": round(sum(r[1] for r in res) / slowest, 1),
     }
+
+
+def _stamp(workload: str, rom_tag: str):
+    """Counter values of the committed rocprofv3 PMC passes of this bench command (profiles/),
+    reported with their source file — they are not measured inside this run."""
+    path = os.path.join(HERE, "profiles", f"pmc_{workload}{rom_tag}.json")
+    if not os.path.exists(path):
+        return None, None
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    return d, os.path.relpath(path, HERE)
 
 
 def main():
@@ -65,13 +105,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
-    ap.add_argument("--workload", choices=["config3", "config2", "config5"], default="config3",
-                    help="config3: rendered screen obs + random actions; config2: headless, fixed action cycle; "
-                         "config5: config3 + reward stack + (72,80,4) obs + per-env reset on done + stats all-reduce")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default=None,
+                    help="default: config3 on one GPU, config4 (the configs[3] per-GPU shard) on several")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: the workload's)")
     ap.add_argument("--actions", choices=["auto", "random", "same"], default="auto",
                     help="override the workload's action stream (diagnostics)")
+    ap.add_argument("--max-episode-steps", type=int, default=None,
+                    help="episode length (config5 default 16, so template reloads happen inside the timed steps)")
     ap.add_argument("--rom", default=None)
+    ap.add_argument("--rom-banks", type=int, default=4, help="pkbench size in 16 KiB banks (4, or 64 = 1 MiB)")
     ap.add_argument("--state", default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -87,28 +129,46 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    wname = args.workload or ("config3" if world == 1 else "config4")
+    W = WORKLOADS[wname]
 
     from pokegym_amd.emulator import BatchedEmulator
     if args.rom:
         rom = open(args.rom, "rb").read()
-        rom_name = os.path.basename(args.rom)
+        rom_name, rom_tag = os.path.basename(args.rom), "_rom"
     else:
         from pokegym_amd.testrom.game import game_rom
-        rom = game_rom()
-        rom_name = "pkbench (synthetic game ROM; pokemon_red.gb is not shipped)"
+        rom = game_rom(banks=args.rom_banks)
+        rom_name = (f"pkbench{'' if args.rom_banks == 4 else args.rom_banks} (synthetic game ROM, {len(rom) // 1024} KiB; "
+                    "pokemon_red.gb is not shipped)")
+        rom_tag = "" if args.rom_banks == 4 else f"_b{args.rom_banks}"
     state = open(args.state, "rb").read() if args.state else None
 
-    render = args.workload in ("config3", "config5")
-    reward = args.workload == "config5"
-    n = args.envs
-    emu = BatchedEmulator(rom, n, state=state, device=local, render=render, reward=reward,
-                          reload_on_reset=reward)
-    if reward:
-        emu.reset()
+    n = args.envs or W["envs"]
+    reward = W["reward"]
+    max_steps = args.max_episode_steps or (16 if reward else 20480)
+    vec = None
+    if W["vecenv"]:
+        from pokegym_amd.env import VecEnv
+        vec = VecEnv(n, rom=rom, state=state, power_on=state is None, device=local, reward=False,
+                     max_episode_steps=max_steps, log_interval=128)
+        emu = vec.emu
+        vec.reset()
+    else:
+        emu = BatchedEmulator(rom, n, state=state, device=local, render=W["render"], reward=reward,
+                              reload_on_reset=reward, max_episode_steps=max_steps)
+        if reward:
+            emu.reset()
     ep_ret = torch.zeros(n, dtype=torch.float64, device=dev)
-    stats = torch.zeros(2, dtype=torch.float64, device=dev)  # [sum of episodic returns, episodes]
+    stats = torch.zeros(3, dtype=torch.float64, device=dev)  # [sum of episodic returns, episodes, resets]
+    rst = [torch.cuda.Event(enable_timing=True) for _ in range(2 * (args.warmup + args.steps))]
+    rst_i = [0]
 
-    def env_step(t):
+    def env_step(t, timed):
+        if vec is not None:
+            vec.send(acts[t])
+            vec.recv()
+            return
         obs, rew, term, trunc = emu.step(acts[t])
         if reward:
             # per-env reload of the template state on done, episodic-return bookkeeping, and the
@@ -118,17 +178,22 @@ def main():
             stats[0] += (ep_ret * d).sum()
             stats[1] += d.sum()
             ep_ret.mul_(1.0 - d)
+            if timed:
+                rst[rst_i[0]].record()
             emu.reset(term)
+            if timed:
+                rst[rst_i[0] + 1].record()
+                rst_i[0] += 2
             if world > 1 and t % 128 == 127:
                 dist.all_reduce(stats)
+
     total = args.warmup + args.steps
-    if args.actions == "same":
-        g = torch.Generator(device=dev)
-        g.manual_seed(1234 + rank)
+    mode = args.actions if args.actions != "auto" else W["actions"]
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)   # Philox counter-based RNG on the device
+    if mode == "same":
         acts = torch.randint(0, 8, (total, 1), generator=g, device=dev).to(torch.uint8).expand(total, n).contiguous()
-    elif args.workload in ("config3", "config5") or args.actions == "random":
-        g = torch.Generator(device=dev)
-        g.manual_seed(1234 + rank)   # Philox counter-based RNG on the device
+    elif mode == "random":
         acts = torch.randint(0, 8, (total, n), generator=g, device=dev, dtype=torch.int64).to(torch.uint8)
     else:
         cyc = torch.tensor([0, 3, 1, 2], dtype=torch.uint8, device=dev)
@@ -136,22 +201,24 @@ def main():
     torch.cuda.synchronize(dev)
 
     for t in range(args.warmup):
-        env_step(t)
+        env_step(t, False)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     emu.profile_enable(True)
+    resets0 = float(stats[1].item())
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    instr = 0
     for t in range(args.warmup, total):
-        env_step(t)
+        env_step(t, True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     emu_ms, ren_ms, rew_ms, nprof = emu.profile_read()
     instr = emu.last_instr_count()  # last step's emulated instructions (all envs)
+    resets = float(stats[1].item()) - resets0
+    k5_ms = sum(rst[2 * i].elapsed_time(rst[2 * i + 1]) for i in range(rst_i[0] // 2))
     t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -162,14 +229,10 @@ def main():
         k1_s = emu_ms / 1e3 / max(nprof, 1)
         k2_s = ren_ms / 1e3 / max(nprof, 1)
         k4_s = rew_ms / 1e3 / max(nprof, 1)
-        achieved = B_HEADLESS * n / k1_s / 1e9
-        traffic = None
-        prof_path = os.path.join(HERE, "profiles", f"pmc_{args.workload}.json")
-        if os.path.exists(prof_path) and not args.rom:
-            try:
-                traffic = json.load(open(prof_path)).get("hbm_bytes_per_launch_k1")
-            except Exception:  # noqa: BLE001
-                traffic = None
+        span_s = k1_s + k2_s + k4_s
+        B = W["bytes"]
+        achieved = B * n / span_s / 1e9
+        stamp, stamp_src = _stamp(wname, rom_tag)
         out = {
             "metric": "aggregate env.step/sec",
             "value": round(value, 1),
@@ -184,27 +247,31 @@ def main():
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": {"config3": "configs[2]: 65536 envs/GPU, PPU-rendered 160x144 u8 screen obs, random actions",
-                             "config2": "configs[1]: headless (no PPU), RAM-only obs, fixed action cycle [0,3,1,2]",
-                             "config5": "configs[4]: configs[2] + full ram_map reward stack + (72,80,4) obs + "
-                                        "per-env template reload on done + episodic-return all-reduce every 128 steps",
-                             }[args.workload],
+                "workload": f"{wname} = {W['desc']}",
                 "envs_per_gpu": n,
+                "envs_total": n * world,
                 "rom": rom_name,
                 "start_state": os.path.basename(args.state) if args.state else "power-on (post-boot)",
                 "frame_skip": 24,
                 "release_frame": 8,
+                "max_episode_steps": max_steps,
                 "parallelism": f"envs sharded over {world} GPU(s), no data-path collective",
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "pk_step_kernel (K1: 24 emulated frames)",
+                "kernel": ("pk_step_kernel (K1, 24 emulated frames) + pk_render_kernel (K2)"
+                           + (" + pk_reward_kernel/pk_obs_kernel (K4/K3)" if reward else "")),
+                "span": "sum of the step's kernel times per env-step (HIP events on the launch stream, "
+                        "averaged over the timed steps); resets excluded",
                 "achieved": round(achieved, 3),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
-                "traffic": traffic,
-                "bytes_per_env_step": B_HEADLESS,
+                "traffic": (stamp or {}).get("hbm_bytes_per_launch_k1"),
+                "traffic_source": (f"{stamp_src}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this "
+                                   "workload (not measured inside this run)") if stamp else None,
+                "bytes_per_env_step": B,
+                "span_ms": round(span_s * 1e3, 3),
                 "k1_ms": round(k1_s * 1e3, 3),
                 "k2_render_ms": round(k2_s * 1e3, 3),
                 "k4_reward_obs_ms": round(k4_s * 1e3, 3),
@@ -212,13 +279,22 @@ def main():
             "emulated_instr_per_s": round(instr / max(k1_s, 1e-9), 1),
             "instr_per_env_step": round(instr / n, 1),
         }
+        if stamp:
+            out["pmc_stamp"] = {k: stamp[k] for k in ("valu_busy_pct", "valu_utilization_pct", "wait_any_pct",
+                                                      "waves_per_simd", "source") if k in stamp}
+        if reward:
+            out["resets"] = {"envs_reset": int(resets), "k5_reset_ms_total": round(k5_ms, 3),
+                             "k5_reset_ms_per_step": round(k5_ms / max(args.steps, 1), 3)}
         if not args.no_cpu_baseline and world == 1:
             try:
                 out["cpu_baseline"] = _cpu_baseline(rom, state)
             except Exception as e:  # noqa: BLE001
                 out["cpu_baseline"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
         print(json.dumps(out), flush=True)
-    emu.close()
+    if vec is not None:
+        vec.close()
+    else:
+        emu.close()
     if world > 1:
         dist.destroy_process_group()
 

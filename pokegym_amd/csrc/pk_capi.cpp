@@ -23,6 +23,7 @@
 hipError_t pk_launch_step(const PkStepArgs& a, hipStream_t s);
 hipError_t pk_launch_render(const PkStepArgs& a, hipStream_t s);
 hipError_t pk_launch_reset(const PkResetArgs& a, hipStream_t s);
+hipError_t pk_launch_list(const uint8_t* mask, uint32_t n, uint32_t* cnt, uint32_t* ids, hipStream_t s);
 hipError_t pk_launch_render_latched(const PkStepArgs& a, hipStream_t s);
 hipError_t pk_launch_gather_env(const uint8_t* mem, uint32_t env, uint8_t* out, hipStream_t s);
 hipError_t pk_launch_gather_range(const uint8_t* mem, uint32_t env0, uint32_t count, uint8_t* out, hipStream_t s);
@@ -250,6 +251,8 @@ struct pk_handle {
     uint32_t* cutc = nullptr;
     uint8_t* obs = nullptr;
     uint8_t* reload = nullptr;
+    // reset lists (pk_list_kernel): [0] reload count, [1] obs count, then npad reload ids, npad obs ids
+    uint32_t* lists = nullptr;
     double* info = nullptr;       // [PK_INFO_NFIELDS][npad]
     uint8_t* info_flag = nullptr; // [npad]
     int32_t* heat = nullptr;      // [npad][444 * 436] (PK_F_HEATMAP)
@@ -294,7 +297,7 @@ void pk_destroy(pk_handle* h) {
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     void* ptrs[] = {h->mem, h->regs, h->lat, h->screen, h->rom, h->ucode, h->bank_slot, h->slot_bank, h->t_mem, h->t_regs,
                     h->t_lat, h->t_screen, h->scratch, h->rs, h->rsd, h->seen, h->mask, h->cutc, h->obs, h->reload,
-                    h->info, h->info_flag, h->heat, h->info_bits};
+                    h->lists, h->info, h->info_flag, h->heat, h->info_bits};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete h;
@@ -322,15 +325,22 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     h->npad = (cfg->n_envs + PK_LANES - 1) / PK_LANES * PK_LANES;
     h->ngroups = h->npad / PK_LANES;
     {
-        // K1 wave shape: 32 envs per wave while that still fits two waves per SIMD (shorter,
-        // less divergent waves; the SIMD interleaves two of them), else 64.  PK_WAVE_LANES overrides.
+        // K1 wave shape (measured, profiles/r02_sweep_*): two waves per SIMD hide part of each
+        // other's memory and LDS latency, so the envs per wave are the largest of 64/32/16 that
+        // still gives two waves per SIMD (65,536 envs -> 32, 32,768 -> 16); below that 32 (one wave
+        // per SIMD on fewer CUs: spreading 4,096 envs over every CU at 4 per wave measured 2.4x
+        // slower — instruction-issue stalls when every CU runs K1).  PK_WAVE_LANES (a power of
+        // two <= 64) overrides.
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device) != hipSuccess || ncu <= 0) ncu = 256;
         h->simds = 4u * (uint32_t)ncu;
-        h->wave_lanes = (h->npad / 32u <= 2u * h->simds) ? 32u : 64u;
+        h->wave_lanes = 32u;
+        for (uint32_t wl = 64u; wl >= 16u; wl >>= 1) {
+            if (h->npad / wl >= 2u * h->simds) { h->wave_lanes = wl; break; }
+        }
         if (const char* wl = getenv("PK_WAVE_LANES")) {
             int v = atoi(wl);
-            if (v != 64 && v != 32 && v != 16) { delete h; return fail(-EINVAL, "PK_WAVE_LANES must be 64, 32 or 16"); }
+            if (v < 1 || v > 64 || (v & (v - 1))) { delete h; return fail(-EINVAL, "PK_WAVE_LANES must be a power of two <= 64"); }
             h->wave_lanes = (uint32_t)v;
         }
         // K1 workgroup size override (parity tests run the benchmarked 512-thread shape at small n):
@@ -374,7 +384,7 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     ALLOC(h->regs, (size_t)PK_NREGS * h->npad * 4);
     ALLOC(h->lat, 3 * h->lat_stride * 4);
     ALLOC(h->screen, (size_t)h->npad * PK_SCREEN);
-    ALLOC(h->rom, cfg->rom_len);
+    ALLOC(h->rom, cfg->rom_len + 16);
     ALLOC(h->ucode, PK_UC_ENTRIES * PK_UE_WORDS * 4);
     ALLOC(h->bank_slot, 128);
     ALLOC(h->slot_bank, PK_LDS_SLOTS);
@@ -383,6 +393,7 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     ALLOC(h->t_lat, 3 * PK_ROWS * 4);
     ALLOC(h->t_screen, PK_SCREEN);
     ALLOC(h->scratch, PK_PHYS + PK_NREGS * 4 + 3 * PK_ROWS * 4 + PK_SCREEN);
+    ALLOC(h->lists, (2 + 2 * (size_t)h->npad) * 4);
     if (h->flags & PK_F_REWARD) {
         ALLOC(h->rs, (size_t)RS_NFIELDS * h->npad * 4);
         ALLOC(h->rsd, (size_t)RSD_NFIELDS * h->npad * 8);
@@ -400,6 +411,7 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     std::vector<uint32_t> uc(PK_UC_ENTRIES * PK_UE_WORDS);
     pk_build_ucode(uc.data());
     hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = hipMemset(h->rom + cfg->rom_len, 0xFF, 16);
     if (e == hipSuccess) e = hipMemcpy(h->rom, cfg->rom, cfg->rom_len, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->ucode, uc.data(), uc.size() * 4, hipMemcpyHostToDevice);
     {
@@ -459,14 +471,18 @@ static PkRewardArgs reward_args(pk_handle* h) {
     return r;
 }
 
-// reload the template state (regs, RAM image, latches, screen) into the masked envs
+// reload the template state (regs, RAM image, latches, screen) into the masked envs: the envs
+// are listed on the device first, so the reset costs in proportion to the envs it touches
 static int template_reset(pk_handle* h, const uint8_t* mask, void* stream) {
     HIPCHK(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipMemsetAsync(h->lists, 0, 4, s));
+    HIPCHK(pk_launch_list(mask, h->n, h->lists, h->lists + 2, s));
     PkResetArgs a;
     a.mem = h->mem; a.regs = h->regs; a.lat = h->lat; a.screen = h->screen;
     a.tmpl_mem = h->t_mem; a.tmpl_regs = h->t_regs; a.tmpl_lat = h->t_lat; a.tmpl_screen = h->t_screen;
-    a.mask = mask; a.n = h->n; a.npad = h->npad; a.lat_stride = (uint32_t)h->lat_stride;
-    HIPCHK(pk_launch_reset(a, (hipStream_t)stream));
+    a.cnt = h->lists; a.ids = h->lists + 2; a.n = h->n; a.npad = h->npad; a.lat_stride = (uint32_t)h->lat_stride;
+    HIPCHK(pk_launch_reset(a, s));
     return 0;
 }
 
@@ -481,6 +497,13 @@ int pk_reset(pk_handle* h, const uint8_t* mask, void* stream) {
     int rc = template_reset(h, h->reload, stream);
     if (rc) return rc;
     HIPCHK(pk_launch_rreset_post(r, s));
+    // the observation of the reset envs only (list of the masked envs)
+    uint32_t* ocnt = h->lists + 1;
+    uint32_t* oids = h->lists + 2 + h->npad;
+    HIPCHK(hipMemsetAsync(ocnt, 0, 4, s));
+    HIPCHK(pk_launch_list(mask, h->n, ocnt, oids, s));
+    r.ocnt = ocnt;
+    r.oids = oids;
     HIPCHK(pk_launch_obs(r, s));
     return 0;
 }
@@ -510,7 +533,7 @@ int pk_set_ram(pk_handle* h, uint16_t addr, uint32_t len, const uint8_t* dense, 
 static PkStepArgs step_args(pk_handle* h, const uint8_t* actions) {
     PkStepArgs a;
     memset(&a, 0, sizeof a);
-    a.mem = h->mem; a.rom = h->rom; a.regs = h->regs; a.ucode = h->ucode; a.actions = actions;
+    a.mem = h->mem; a.rom = h->rom; a.romw = reinterpret_cast<const uint32_t*>(h->rom); a.regs = h->regs; a.ucode = h->ucode; a.actions = actions;
     a.lat = h->lat; a.screen = h->screen; a.n = h->n; a.npad = h->npad;
     a.rom_bank_mask = h->bank_mask; a.mbc = h->mbc; a.frames = h->frames;
     a.release_frame = h->release; a.render_last = (h->flags & PK_F_RENDER) ? 1 : 0;

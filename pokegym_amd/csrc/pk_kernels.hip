@@ -63,37 +63,39 @@ __global__ void __launch_bounds__(256) pk_arm_latches_kernel(PkStepArgs A) {
 // K5: reset selected envs from the template (regs + RAM image + screen + line latches).
 
 
+// The reset kernels work on a device-built list of the envs to reset (pk_list_kernel: ids of the
+// masked envs, count in device memory), so a step where few or no envs finish costs a few
+// near-empty launches instead of a scan of every env's 49.7 KB image — and no host sync.
+__global__ void __launch_bounds__(256) pk_list_kernel(const u8* mask, u32 n, u32* cnt, u32* ids) {
+    const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n || (mask && !mask[e])) return;
+    ids[atomicAdd(cnt, 1u)] = e;
+}
+
+// template RAM image -> listed envs: thread = env (list order, so a wave's stores to one image
+// row land in one 64-byte line when its envs share a group), block = a strided set of rows
 __global__ void __launch_bounds__(256) pk_reset_mem_kernel(PkResetArgs A) {
-    // grid-stride over (group, phys/16): each thread writes 16 lanes' bytes of one phys row? No:
-    // one thread = one (env, 16 consecutive phys bytes)
-    const size_t total = (size_t)A.npad * (PK_PHYS / 16u);
-    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
-        // t enumerates (gid, row16, lane) with lane fastest so that stores are coalesced
-        u32 lane = (u32)(t % PK_LANES);
-        size_t r = t / PK_LANES;
-        u32 chunk = (u32)(r % (PK_PHYS / 16u));
-        u32 gid = (u32)(r / (PK_PHYS / 16u));
-        u32 env = gid * PK_LANES + lane;
-        if (env >= A.n) continue;
-        if (A.mask && !A.mask[env]) continue;
-        u8* g = A.mem + (size_t)gid * PK_GROUP_STRIDE;
-        const u8* src = A.tmpl_mem + chunk * 16u;
-        for (u32 k = 0; k < 16u; k++) g[(chunk * 16u + k) * PK_LANES + lane] = src[k];
+    const u32 cnt = *A.cnt;
+    for (u32 k = threadIdx.x; k < cnt; k += blockDim.x) {
+        const u32 env = A.ids[k];
+        u8* g = A.mem + (size_t)(env / PK_LANES) * PK_GROUP_STRIDE + env % PK_LANES;
+        for (u32 p = blockIdx.x; p < PK_PHYS; p += gridDim.x) g[(size_t)p * PK_LANES] = A.tmpl_mem[p];
     }
 }
 
 __global__ void __launch_bounds__(256) pk_reset_regs_kernel(PkResetArgs A) {
-    const u32 env = blockIdx.x * blockDim.x + threadIdx.x;
-    if (env >= A.n) return;
-    if (A.mask && !A.mask[env]) return;
-    for (u32 f = 0; f < PK_NREGS; f++) A.regs[f * A.npad + env] = A.tmpl_regs[f];
-    const u32 gid = env / PK_LANES, lane = env % PK_LANES;
-    for (u32 k = 0; k < 3u; k++)
-        for (u32 y = 0; y < PK_ROWS; y++)
-            A.lat[k * A.lat_stride + (gid * PK_ROWS + y) * PK_LANES + lane] = A.tmpl_lat[k * PK_ROWS + y];
-    const uint4* s = reinterpret_cast<const uint4*>(A.tmpl_screen);
-    uint4* d = reinterpret_cast<uint4*>(A.screen + (size_t)env * PK_SCREEN);
-    for (u32 q = 0; q < PK_SCREEN / 16u; q++) d[q] = s[q];
+    const u32 cnt = *A.cnt;
+    for (u32 k = blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += gridDim.x * blockDim.x) {
+        const u32 env = A.ids[k];
+        for (u32 f = 0; f < PK_NREGS; f++) A.regs[f * A.npad + env] = A.tmpl_regs[f];
+        const u32 gid = env / PK_LANES, lane = env % PK_LANES;
+        for (u32 j = 0; j < 3u; j++)
+            for (u32 y = 0; y < PK_ROWS; y++)
+                A.lat[j * A.lat_stride + (gid * PK_ROWS + y) * PK_LANES + lane] = A.tmpl_lat[j * PK_ROWS + y];
+        const uint4* s = reinterpret_cast<const uint4*>(A.tmpl_screen);
+        uint4* d = reinterpret_cast<uint4*>(A.screen + (size_t)env * PK_SCREEN);
+        for (u32 q = 0; q < PK_SCREEN / 16u; q++) d[q] = s[q];
+    }
 }
 
 // gather one env's RAM image into a compact buffer (for pk_snapshot / pk_peek)
@@ -137,8 +139,14 @@ hipError_t pk_launch_render_latched(const PkStepArgs& a, hipStream_t s) {
     return pk_launch_render(a, s);
 }
 
+hipError_t pk_launch_list(const u8* mask, u32 n, u32* cnt, u32* ids, hipStream_t s) {
+    hipLaunchKernelGGL(pk_list_kernel, dim3((n + 255) / 256), dim3(256), 0, s, mask, n, cnt, ids);
+    return hipGetLastError();
+}
+
+// reset the envs listed in (a.cnt, a.ids)
 hipError_t pk_launch_reset(const PkResetArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(pk_reset_mem_kernel, dim3(2048), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(pk_reset_mem_kernel, dim3(4096), dim3(256), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(pk_reset_regs_kernel, dim3((a.npad + 255) / 256), dim3(256), 0, s, a);

@@ -66,7 +66,8 @@ enum {
 // kernel argument blocks (passed by value)
 struct PkStepArgs {
     uint8_t* mem;             // lane-interleaved RAM images
-    const uint8_t* rom;       // whole ROM
+    const uint8_t* rom;       // whole ROM (+16 bytes of padding: dword fetches may overrun the end)
+    const uint32_t* romw;     // the same, as dwords
     uint32_t* regs;           // SoA lane registers [PK_NREGS][npad]
     const uint32_t* ucode;    // microcode table (pk_ucode.h), PK_UC_ENTRIES x 8 dwords
     const uint8_t* actions;   // [n] action ids (0..7; >=8 = no button)
@@ -96,6 +97,7 @@ struct PkResetArgs {
     const uint32_t* tmpl_regs;   // PK_NREGS
     const uint32_t* tmpl_lat;    // 3*144
     const uint8_t* tmpl_screen;  // 144*160
-    const uint8_t* mask;         // [n] or null = all
+    const uint32_t* cnt;         // envs to reset: count (device memory) ...
+    const uint32_t* ids;         // ... and their ids (pk_list_kernel)
     uint32_t n, npad, lat_stride;
 };

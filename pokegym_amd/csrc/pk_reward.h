@@ -93,6 +93,8 @@ struct PkRewardArgs {
     uint8_t* reload;          // reset: [n] out = template reload wanted
     const uint8_t* screen;    // [npad][144][160] grey
     uint8_t* obs;             // [n][72][80][4]
+    const uint32_t* ocnt;     // obs for listed envs only (reset): count (device memory) and ids,
+    const uint32_t* oids;     // or null = all n envs
     double* rew;              // [n] or null
     uint8_t* term;            // [n] or null
     uint8_t* trunc;           // [n] or null

@@ -685,12 +685,15 @@ __global__ void __launch_bounds__(256) pk_rreset_post_kernel(PkRewardArgs A) {
 // ---------------------------------------------------------------------------------------------
 // K3: obs (72, 80, 4) = screen[::2, ::2] x 3 channels + mask window centred on (r, c).
 // One thread = 4 consecutive pixels (one 16-byte store); grid-stride over (env, row, quad).
+// With a list (A.ocnt/A.oids: the envs a reset touched) only those envs are rebuilt.
 __global__ void __launch_bounds__(256) pk_obs_kernel(PkRewardArgs A) {
-    const size_t total = (size_t)A.n * PK_OBS_H * (PK_OBS_W / 4u);
+    const u32 cnt = A.ocnt ? *A.ocnt : A.n;
+    const size_t total = (size_t)cnt * PK_OBS_H * (PK_OBS_W / 4u);
     for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
         const u32 q = (u32)(t % (PK_OBS_W / 4u));
         const u32 y = (u32)((t / (PK_OBS_W / 4u)) % PK_OBS_H);
-        const u32 e = (u32)(t / ((size_t)PK_OBS_H * (PK_OBS_W / 4u)));
+        const u32 k = (u32)(t / ((size_t)PK_OBS_H * (PK_OBS_W / 4u)));
+        const u32 e = A.oids ? A.oids[k] : k;
         const u8* g = A.mem + (size_t)(e / PK_LANES) * PK_GROUP_STRIDE + (e % PK_LANES);
         const int r = g[(size_t)(PK_P_WRAM + 0x1361u) * PK_LANES];
         const int c = g[(size_t)(PK_P_WRAM + 0x1362u) * PK_LANES];

@@ -128,6 +128,10 @@ __device__ __forceinline__ bool vram_or_oam(u32 a) { return (a >= 0x8000u && a <
 // ROM address staged in LDS?  and its LDS byte index
 __device__ __forceinline__ bool rom_staged(const St& s, u32 a) { return a < 0x4000u || (a < 0x8000u && s.rb != PK_NO_BANK); }
 __device__ __forceinline__ u32 rom_lds_index(const St& s, u32 a) { return sel(a < 0x4000u, a, s.rb + (a & 0x3FFFu)); }
+// byte index in the global ROM of a switchable-bank address (0x4000-0x7FFF)
+__device__ __forceinline__ u32 rom_global_index(const PkStepArgs& A, const St& s, u32 a) {
+    return (((s.mbc & 0xFFu) & A.rom_bank_mask) << 14) | (a & 0x3FFFu);
+}
 __device__ __forceinline__ u32 slot_base(u32 bank) {
     const int sl = lds_slot[bank & 127u];
     return sl >= 0 ? (u32)sl * 0x4000u : PK_NO_BANK;
@@ -358,7 +362,13 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
 
     // thread -> env: the first wave_lanes lanes of each wave carry envs (fewer envs per wave =
     // more waves per SIMD for the same env count); the RAM layout is unchanged.
-    const u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
+    // XCD-aware workgroup order: the hardware hands workgroup b to XCD b % 8, and each XCD has its
+    // own L2.  When a workgroup holds fewer than 64 envs (few envs per wave), one 64-env image
+    // group spans several workgroups; numbering them XCD-major keeps those on one XCD, so a
+    // group's cache lines live in one L2 instead of bouncing between eight.
+    const u32 G = gridDim.x, G8 = G & ~7u;
+    const u32 blk = blockIdx.x < G8 ? (blockIdx.x & 7u) * (G8 >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+    const u32 tid = blk * blockDim.x + threadIdx.x;
     const u32 wl = tid & (PK_LANES - 1u);
     if (wl >= A.wave_lanes) return;
     const u32 env = (tid >> 6) * A.wave_lanes + wl;
@@ -462,6 +472,12 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
                     const u32 p = fast_phys(pc);
                     bytes = ld_img(c, p) | (ld_img(c, p + 1u) << 8) | (ld_img(c, p + 2u) << 16);
                     ev |= PK_EV_F_BUS | sel(pc >= 0xFF80u, PK_EV_HRAM, 0u);
+                } else if (pc - 0x4000u < 0x3FFEu) {
+                    // switchable bank not staged in LDS (a 64-bank cartridge runs most banks from
+                    // here): two aligned dwords of the global ROM (1 MiB, L2-resident)
+                    const u32 ga = rom_global_index(A, s, pc);
+                    bytes = __builtin_amdgcn_alignbyte(A.romw[(ga >> 2) + 1u], A.romw[ga >> 2], ga & 3u);
+                    ev |= PK_EV_F_ROM16;
                 } else {
                     const St t = s;
                     bytes = pk_fetch_slow(&A, c.g, c.lane, c.loc, &t, pc);
@@ -528,6 +544,10 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             if (!rd2 & (addr0 >= 0xFF00u) & ((addr0 < 0xFF80u) | (addr0 == 0xFFFFu))) {
                 xm = io_read(c, s, addr0);
                 ev |= PK_EV_RD_IO;
+            } else if ((addr0 - 0x4000u < 0x4000u) & pair) {  // unstaged switchable bank: the global ROM
+                const u32 ga = rom_global_index(A, s, addr0);
+                xm = A.rom[ga] | sel(rd2, (u32)A.rom[ga + (u32)sfield(D, PK_DB_ADIR, 2)] << 8, 0u);
+                ev |= PK_EV_RD_ROMG;
             } else {
                 const St t = s;
                 xm = pk_read_slow(&A, c.g, c.lane, c.loc, &t, addr0, addr1, rd2 ? 1u : 0u);

@@ -113,18 +113,25 @@ class VecEnv:
     def __init__(self, num_envs: int, rom_path=None, state_path=None, rom: bytes | None = None, state: bytes | None = None,
                  device: int | None = None, max_episode_steps: int = 20480, reward_scale: float = 4.0,
                  reload_on_reset: bool = False, env_offset: int = 0, log_interval: int = 128, emulator=None,
-                 heatmap: bool = False):
+                 heatmap: bool = False, reward: bool = True, power_on: bool = False):
+        """reward=False: the screen-obs env of configs[3] — obs is the (144, 160) u8 screen, rewards are
+        0 and episodes end at max_episode_steps.  power_on=True starts (and resets) every env from
+        the cartridge's power-on state instead of a savestate."""
         if emulator is None:
             from .emulator import BatchedEmulator
             rom = rom if rom is not None else _read(rom_path or "pokemon_red.gb")
-            state = state if state is not None else _read(state_path if state_path is not None else DEFAULT_STATE)
+            if power_on:
+                state = None
+            else:
+                state = state if state is not None else _read(state_path if state_path is not None else DEFAULT_STATE)
             emulator = BatchedEmulator(rom, num_envs, state=state, device=0 if device is None else device, render=True,
-                                       reward=True, max_episode_steps=max_episode_steps, reward_scale=reward_scale,
+                                       reward=reward, max_episode_steps=max_episode_steps, reward_scale=reward_scale,
                                        reload_on_reset=reload_on_reset, heatmap=heatmap)
         self.emu = emulator
         self.device = emulator.device
         self.num_envs = self.num_agents = num_envs
-        self.single_observation_space = spaces.observation_space()
+        self.single_observation_space = (spaces.observation_space() if getattr(emulator, "reward", True)
+                                         else spaces.screen_space())
         self.single_action_space = spaces.action_space()
         self.env_ids = torch.arange(env_offset, env_offset + num_envs, device=self.device)
         self.masks = torch.ones(num_envs, dtype=torch.bool, device=self.device)

@@ -39,3 +39,9 @@ def observation_space():
 
 def action_space():
     return Discrete(8)
+
+
+def screen_space():
+    """The full-resolution grey screen (screen.screen_ndarray()[:, :, 0], environment.py:268) that
+    the screen-obs configuration returns instead of the (72, 80, 4) composite."""
+    return Box(low=0, high=255, shape=(144, 160), dtype=np.uint8)

@@ -17,6 +17,8 @@ Everything is deterministic given the action stream; per-env divergence comes fr
 """
 from __future__ import annotations
 
+import re
+
 from .sm83asm import build_rom
 
 SRC = r"""
@@ -1075,5 +1077,131 @@ divide16:
 """
 
 
-def game_rom() -> bytes:
-    return build_rom(SRC, n_banks=4, title="PKBENCH")
+# Routines the banked variant relocates out of the home bank (pokered keeps its overworld engine,
+# map scripts and text in many switchable banks and reaches them through Bankswitch every frame).
+# prepare_oam / put_tile stay home: the VBlank handler calls them with any bank mapped.
+BANKED_ROUTINES = ("update_npcs", "update_sprites", "draw_map_view", "text_engine", "menu_logic")
+FIRST_OW_BANK = 4
+
+
+def _routines(src: str) -> dict[str, str]:
+    """Global-label spans of the home bank (label line up to the next global label)."""
+    home = src[:src.index("section 2")]
+    marks = [(m.start(), m.group(1)) for m in re.finditer(r"^([A-Za-z_]\w*):", home, re.M)]
+    marks.append((len(home), None))
+    return {name: home[a:b] for (a, name), (b, _) in zip(marks, marks[1:])}
+
+
+def banked_source(n_banks: int) -> str:
+    """`pkbench` re-laid-out for an n_banks cartridge (64 = 1 MiB, pokemon_red.gb's size): the
+    overworld engine (NPCs, sprite state, map view, text, menu) plus a per-bank map script lives in
+    banks FIRST_OW_BANK..n_banks-1, one copy per bank; every frame the main loop picks the bank of
+    the player's 4x4-metatile region, (x/4 + 16*(y/4)) mod (n_banks - 4), and reaches its engine
+    through a Bankswitch trampoline (save hROMBank, switch, call $4000, restore), so envs in
+    different regions run code from different banks and most executed code sits outside the six
+    banks K1 stages in LDS."""
+    nb = n_banks - FIRST_OW_BANK
+    spans = _routines(SRC)
+    home = SRC[:SRC.index("section 2")]
+    for name in BANKED_ROUTINES:
+        home = home.replace(spans[name], "")
+    main_old = """    call update_npcs
+    call update_sprites
+    ld a, [wMoved]
+    and a
+    call nz, draw_map_view
+    call text_engine
+    call menu_logic
+"""
+    main_new = f"""    ; region -> bank: 4 + (x/4 + 16*(y/4)) mod {nb}
+    ld a, [wPlayerX]
+    rrca
+    rrca
+    and $0f
+    ld b, a
+    ld a, [wPlayerY]
+    add a, a
+    add a, a
+    and $f0
+    or b
+.mod:
+    cp {nb}
+    jr c, .inr
+    sub {nb}
+    jr .mod
+.inr:
+    add a, {FIRST_OW_BANK}
+    call farcall_ow
+"""
+    assert main_old in home
+    home = home.replace(main_old, main_new)
+    home = home.replace("farcall_battle:", """farcall_ow:
+    ; pokered Bankswitch into the region's overworld bank: the engine entry is at $4000
+    ld b, a
+    ldh a, [hROMBank]
+    push af
+    ld a, b
+    ldh [hROMBank], a
+    ld [$2000], a
+    call $4000
+    pop af
+    ldh [hROMBank], a
+    ld [$2000], a
+    ret
+
+farcall_battle:""")
+    out = [home, SRC[SRC.index("section 2"):]]
+    for b in range(FIRST_OW_BANK, n_banks):
+        body = "".join(spans[name] for name in BANKED_ROUTINES)
+        for name in BANKED_ROUTINES:
+            body = re.sub(rf"\b{name}\b", f"{name}_b{b}", body)
+        # a map script per bank: fold 16 bytes of this bank's table (chosen by the frame counter)
+        # into wMathR — data reads from the switched bank, like pokered's map headers and text
+        table = ", ".join(f"${(b * 37 + k * 11) & 0xFF:02x}" for k in range(32))
+        out.append(f"""
+section {b}
+org $4000
+ow_entry_b{b}:
+    call update_npcs_b{b}
+    call update_sprites_b{b}
+    ld a, [wMoved]
+    and a
+    call nz, draw_map_view_b{b}
+    call text_engine_b{b}
+    call menu_logic_b{b}
+    ldh a, [hFrameCounter]
+    and $0f
+    ld hl, script_table_b{b}
+    add a, l
+    ld l, a
+    ld a, h
+    adc a, 0
+    ld h, a
+    ld a, [wMathR]
+    ld c, a
+    ld b, 16
+.s:
+    ld a, [hl+]
+    xor c
+    rlca
+    ld c, a
+    dec b
+    jr nz, .s
+    ld a, c
+    ld [wMathR], a
+    ret
+{body}
+script_table_b{b}:
+    db {table}
+""")
+    return "".join(out)
+
+
+def game_rom(banks: int = 4) -> bytes:
+    """pkbench: banks=4 is the benchmark ROM of round 1 (every bank fits the LDS staging);
+    banks=64 is the 1 MiB layout with the overworld engine spread over 60 switchable banks."""
+    if banks == 4:
+        return build_rom(SRC, n_banks=4, title="PKBENCH")
+    if banks < 8 or banks & (banks - 1) or banks > 128:
+        raise ValueError("banks must be 4 or a power of two in [8, 128]")
+    return build_rom(banked_source(banks), n_banks=banks, title=f"PKBENCH{banks}")

@@ -80,10 +80,10 @@ def test_load_snapshot_roundtrip():
     emu.close()
 
 
-@pytest.mark.parametrize("lanes", ["64", "32", "16"])
+@pytest.mark.parametrize("lanes", ["64", "32", "16", "4", "1"])
 def test_game_rom_parity_wave_shapes(lanes, monkeypatch):
     """The pkbench game (HALT/VBlank frame loop, HRAM OAM-DMA routine, MBC3 banking, SRAM) under
-    every K1 wave shape: 64, 32 or 16 envs per wave (PK_WAVE_LANES), with random actions."""
+    every K1 wave shape: 64, 32, 16, 4 or 1 envs per wave (PK_WAVE_LANES), with random actions."""
     from pokegym_amd.testrom.game import game_rom
     monkeypatch.setenv("PK_WAVE_LANES", lanes)
     rom = game_rom()
@@ -104,6 +104,31 @@ def test_fuzz_rom_parity_512_thread_workgroups(seed, render, monkeypatch):
     rom = game_rom() if seed < 0 else fuzz_rom(seed)
     n, steps = 256, 8
     gpu, ref = _run_both(rom, None, n, steps, 100 + seed, render=render)
+    g = np.frombuffer(b"".join(gpu), np.uint8).reshape(n, -1)
+    a = oracle.state_digests(g, headless=not render)
+    b = oracle.state_digests(ref, headless=not render)
+    bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in np.nonzero(a != b)[0][:4]]
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("seed", [2, 13, 40])
+def test_fuzz_rom_parity_64_banks(seed):
+    """1 MiB fuzz cartridges: code and data in the 58 switchable banks K1 does not stage in LDS
+    (global-ROM fetch and read paths)."""
+    rom = fuzz_rom(seed, n_banks=64)
+    n, steps = 128, 12
+    gpu, ref = _run_both(rom, None, n, steps, 200 + seed)
+    bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
+    assert not bad, bad[:4]
+
+
+@pytest.mark.parametrize("render", [True, False])
+def test_game_rom_64_banks_parity(render):
+    """pkbench on the 64-bank layout (overworld engine in 60 switchable banks), 512 envs."""
+    from pokegym_amd.testrom.game import game_rom
+    rom = game_rom(64)
+    n, steps = 512, 10
+    gpu, ref = _run_both(rom, None, n, steps, 64, render=render)
     g = np.frombuffer(b"".join(gpu), np.uint8).reshape(n, -1)
     a = oracle.state_digests(g, headless=not render)
     b = oracle.state_digests(ref, headless=not render)

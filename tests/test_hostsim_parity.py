@@ -31,3 +31,15 @@ def test_hostsim_region_seams():
     """16-bit accesses across the RAM region seams take the generic bus path (K1 pair rule)."""
     from pokegym_amd.testrom.fuzz import boundary_rom
     assert check(boundary_rom(), 8, 2, 9) == []
+
+
+@pytest.mark.parametrize("seed", [2, 13, 40])
+def test_hostsim_fuzz_64_banks(seed):
+    """1 MiB fuzz cartridges: code and data in the 58 switchable banks K1 does not stage in LDS
+    (global-ROM fetch and read paths)."""
+    assert check(fuzz_rom(seed, n_banks=64), 8, 3, seed) == []
+
+
+def test_hostsim_game_64_banks():
+    """pkbench on the 64-bank layout (overworld engine in 60 banks behind Bankswitch trampolines)."""
+    assert check(game_rom(64), 8, 8, 5) == []
