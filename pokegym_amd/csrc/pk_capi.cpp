@@ -253,6 +253,7 @@ struct pk_handle {
     uint8_t* reload = nullptr;
     // reset lists (pk_list_kernel): [0] reload count, [1] obs count, then npad reload ids, npad obs ids
     uint32_t* lists = nullptr;
+    unsigned long long* dbg = nullptr;  // K1 phase-cycle counters of a -DPK_STAMP build
     double* info = nullptr;       // [PK_INFO_NFIELDS][npad]
     uint8_t* info_flag = nullptr; // [npad]
     int32_t* heat = nullptr;      // [npad][444 * 436] (PK_F_HEATMAP)
@@ -297,7 +298,7 @@ void pk_destroy(pk_handle* h) {
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     void* ptrs[] = {h->mem, h->regs, h->lat, h->screen, h->rom, h->ucode, h->bank_slot, h->slot_bank, h->t_mem, h->t_regs,
                     h->t_lat, h->t_screen, h->scratch, h->rs, h->rsd, h->seen, h->mask, h->cutc, h->obs, h->reload,
-                    h->lists, h->info, h->info_flag, h->heat, h->info_bits};
+                    h->lists, h->dbg, h->info, h->info_flag, h->heat, h->info_bits};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete h;
@@ -394,6 +395,10 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     ALLOC(h->t_screen, PK_SCREEN);
     ALLOC(h->scratch, PK_PHYS + PK_NREGS * 4 + 3 * PK_ROWS * 4 + PK_SCREEN);
     ALLOC(h->lists, (2 + 2 * (size_t)h->npad) * 4);
+#ifdef PK_STAMP
+    ALLOC(h->dbg, 64 * 8);
+    (void)hipMemset(h->dbg, 0, 64 * 8);
+#endif
     if (h->flags & PK_F_REWARD) {
         ALLOC(h->rs, (size_t)RS_NFIELDS * h->npad * 4);
         ALLOC(h->rsd, (size_t)RSD_NFIELDS * h->npad * 8);
@@ -542,6 +547,7 @@ static PkStepArgs step_args(pk_handle* h, const uint8_t* actions) {
     a.wave_lanes = h->wave_lanes;
     a.simds = h->simds;
     a.block = h->k1_block;
+    a.dbg = h->dbg;
     return a;
 }
 
@@ -802,6 +808,18 @@ int pk_profile_read(pk_handle* h, double* emu_ms, double* render_ms, double* rew
     *reward_ms = c;
     *steps = n;
     h->ev_used = 0;
+    return 0;
+}
+
+// diagnostic: the K1 phase-cycle counters of a -DPK_STAMP build (zeros otherwise), then reset
+int pk_debug_counters(pk_handle* h, uint64_t* out, uint32_t n) {
+    if (!h || !out) return fail(-EINVAL, "null argument");
+    memset(out, 0, (size_t)n * 8);
+    if (!h->dbg) return 0;
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(out, h->dbg, (size_t)(n < 64 ? n : 64) * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemset(h->dbg, 0, 64 * 8));
     return 0;
 }
 

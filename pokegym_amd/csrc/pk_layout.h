@@ -86,6 +86,7 @@ struct PkStepArgs {
     uint32_t wave_lanes;      // envs per 64-lane wave in K1 (64, 32 or 16): fewer lanes = more waves/SIMD
     uint32_t simds;           // SIMDs of the device: K1 uses 256-thread workgroups while waves <= simds
     uint32_t block;           // K1 workgroup size override (0 = by geometry; PK_K1_BLOCK, tests)
+    unsigned long long* dbg;  // diagnostic counters (-DPK_STAMP builds only), else null
 };
 
 struct PkResetArgs {

@@ -48,6 +48,19 @@
 #ifndef PK_ITER
 #define PK_ITER(env, ev) ((void)(ev))
 #endif
+// diagnostic build only (-DPK_STAMP, tools/stamp_build.py): per-phase wave cycles of the loop,
+// read with s_memtime at points where the loop already waits, summed per wave into A.dbg
+#ifdef PK_STAMP
+#define PK_NSTAMP 5
+#define PK_STAMP_AT(k)                                          \
+    do {                                                        \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();       \
+        st_acc[k] += (uint64_t)(t_ - st_prev);                  \
+        st_prev = t_;                                           \
+    } while (0)
+#else
+#define PK_STAMP_AT(k) ((void)0)
+#endif
 enum {
     PK_EV_EXEC = 1u << 0, PK_EV_F_LDS = 1u << 1, PK_EV_F_ROM16 = 1u << 2, PK_EV_F_BUS = 1u << 3,
     PK_EV_INT = 1u << 4, PK_EV_IDLE = 1u << 5, PK_EV_RD = 1u << 6, PK_EV_RD_ROMLDS = 1u << 7,
@@ -298,7 +311,22 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
                     s.npend = 0;
                 }
                 const u32 src = v << 8;
-                for (u32 n = 0; n < 0xA0u; n++) st_img(c, PK_P_OAM + n, bus_read_any(c, s, (src + n) & 0xFFFFu));
+                if (fast_ram(src) && src < 0xFE00u) {
+                    // plain RAM page (VRAM, WRAM, echo: the OAM buffers games use): the page is
+                    // linear in the image, so copy in batches of 32 independent loads — the
+                    // byte-by-byte bus loop waited one memory round trip per byte, and one lane
+                    // in DMA held its whole wave for ~160 of them
+                    const u32 sp = fast_phys(src);
+                    for (u32 n0 = 0; n0 < 0xA0u; n0 += 32u) {
+                        u32 b[32];
+#pragma unroll
+                        for (u32 k = 0; k < 32u; k++) b[k] = ld_img(c, sp + n0 + k);
+#pragma unroll
+                        for (u32 k = 0; k < 32u; k++) st_img(c, PK_P_OAM + n0 + k, b[k]);
+                    }
+                } else {
+                    for (u32 n = 0; n < 0xA0u; n++) st_img(c, PK_P_OAM + n, bus_read_any(c, s, (src + n) & 0xFFFFu));
+                }
                 break;
             }
             case 0xFF47: s.lcd2 = setb8(s.lcd2, 0, v); break;
@@ -432,8 +460,15 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
     // seen) while the timer/LCD work runs; pf = 0 -> fetch and decode at the top instead
     u32 pf = 0, pbytes = 0;
     uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0, p2 = p0;
+#ifdef PK_STAMP
+    uint64_t st_acc[PK_NSTAMP] = {0, 0, 0, 0, 0}, st_prev = __builtin_amdgcn_s_memtime(), st_iter = 0;
+#endif
     while (frame < A.frames) {
         u32 ev = 0;
+        PK_STAMP_AT(4);
+#ifdef PK_STAMP
+        st_iter++;
+#endif
         // ---------------- front-end: cpu.tick / check_interrupts ----------------
         // common case (running, nothing pending): execute at pc; otherwise the full PyBoy order
         const u32 cpu0 = s.cpu;
@@ -559,6 +594,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
                       | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
                       | sel(addr0 >= 0xC000u && addr0 < 0xFE00u, PK_EV_RD_WRAM, 0u), 0u);
         const u32 m16 = m0 | (m1 << 8);
+        PK_STAMP_AT(0);
 
         // ---------------- fused datapath ----------------
         const u32 q1 = m16 | (sp << 16);
@@ -655,6 +691,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         ev |= sel(wr, PK_EV_WR | sel(wr2, PK_EV_WR2, 0u) | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
                       | sel(addr0 >= 0xC000u && addr0 < 0xFE00u, PK_EV_WR_WRAM, sel(addr0 >= 0x8000u && addr0 < 0xA000u, PK_EV_WR_VRAM, 0u)), 0u);
 
+        PK_STAMP_AT(1);
         // ---------------- prefetch the next instruction (LDS-staged ROM or the HRAM mirror) ----------------
         {
             const u32 npc = s.pc;
@@ -667,6 +704,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
                 pbytes = lds_hcode[q] | (lds_hcode[q + PK_WG_ENVS] << 8) | (lds_hcode[q + 2u * PK_WG_ENVS] << 16);
             }
             const u32 op = pbytes & 0xFFu;
+            PK_STAMP_AT(2);
             const u32 di = sel(op == 0xCBu, 256u + ((pbytes >> 8) & 0xFFu), op);
             p0 = ucv[di * 3u];
             p1 = ucv[di * 3u + 1u];
@@ -782,6 +820,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             s.blank |= s.render;
         }
         s.cpu |= irq << 16;
+        PK_STAMP_AT(3);
         budget += cycles + 1u;
         ev |= sel(s.frame_done != 0u || budget > 16u * FRAME_CYCLES, PK_EV_FRAME, 0u);
         PK_ITER(env, ev);
@@ -798,6 +837,13 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         }
     }
 
+#ifdef PK_STAMP
+    if (A.dbg && wl == 0u) {
+        for (int k = 0; k < PK_NSTAMP; k++) atomicAdd(&A.dbg[k], (unsigned long long)st_acc[k]);
+        atomicAdd(&A.dbg[PK_NSTAMP], (unsigned long long)st_iter);
+        atomicAdd(&A.dbg[PK_NSTAMP + 1], 1ull);
+    }
+#endif
     if (!active) return;
     lcd_unfold(s);
     R[PK_R_W0 * np + env] = s.w0;

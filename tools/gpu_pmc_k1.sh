@@ -18,6 +18,16 @@ for spec in "$@"; do
     env $envs timeout -k 10 300 rocprofv3 --kernel-trace --pmc "$@" -d $OUT/${name}_$p -o $p --output-format csv -- \
       python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline $args > $OUT/${name}_$p.json 2> $OUT/${name}_$p.err
   }
+  if [ -n "$MEMPASS" ]; then
+    run c TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_LATENCY_sum TCP_TCC_WRITE_REQ_sum TCC_HIT_sum TCC_MISS_sum && \
+    run d TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TCP_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum || { rc=$?; break; }
+    continue
+  fi
+  if [ -n "$ISSUEPASS" ]; then
+    run e SQ_IFETCH SQC_ICACHE_MISSES SQC_ICACHE_HITS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR && \
+    run f SQ_ACTIVE_INST_VALU2 SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_FLAT SQ_INST_CYCLES_SALU SQ_INSTS_SMEM SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY || { rc=$?; break; }
+    continue
+  fi
   run a SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE GRBM_COUNT && \
   run b SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INSTS_BRANCH || { rc=$?; break; }
 done
