@@ -25,14 +25,15 @@ __global__ void __launch_bounds__(64) pk_render_kernel(PkStepArgs A) {
     if (env >= A.n) return;
     const u32 rf = A.regs[PK_R_RFLAGS * A.npad + env];
     u8* out = A.screen + (size_t)env * PK_SCREEN + y * PK_COLS;
-    if (rf & 1u) {  // frame ended with the LCD off: blank_screen() (white)
+    const u32 idx = (gid * PK_ROWS + y) * PK_LANES + lane;
+    const u32 l2 = A.lat[2u * A.lat_stride + idx];
+    if (rf & 1u) {  // frame ended with the LCD off: blank_screen() (white); its latched lines are dropped
         uint4 wv;
         wv.x = wv.y = wv.z = wv.w = 0xFFFFFFFFu;
         for (u32 q = 0; q < PK_COLS; q += 16) *reinterpret_cast<uint4*>(out + q) = wv;
+        if (l2 & 0x100u) A.lat[2u * A.lat_stride + idx] = l2 & ~0x100u;
         return;
     }
-    const u32 idx = (gid * PK_ROWS + y) * PK_LANES + lane;
-    const u32 l2 = A.lat[2u * A.lat_stride + idx];
     if (!(l2 & 0x100u)) return;
     Mem m;
     m.g = A.mem + (size_t)gid * PK_GROUP_STRIDE;

@@ -140,12 +140,18 @@ __device__ __noinline__ static void flush_lines(u32* lat, u32 lat_stride, u8* sc
     u32* lat0 = lat;
     u32* lat1 = lat + lat_stride;
     u32* lat2 = lat + 2u * lat_stride;
-    for (u32 y = 0; y < PK_ROWS; y++) {
-        u32 idx = (gid * PK_ROWS + y) * PK_LANES + lane;
-        u32 l2 = lat2[idx];
-        if (l2 & 0x100u) {
-            render_line(m, y, lat0[idx], lat1[idx], (int)(l2 & 0xFFu) - 1, screen + (size_t)env * PK_SCREEN + y * PK_COLS);
-            lat2[idx] = l2 & ~0x100u;
+    // the latch flags are read 16 lines at a time (independent loads: one memory round trip per
+    // batch instead of one per line)
+    for (u32 y0 = 0; y0 < PK_ROWS; y0 += 16u) {
+        u32 f[16];
+#pragma unroll
+        for (u32 k = 0; k < 16u; k++) f[k] = lat2[(gid * PK_ROWS + y0 + k) * PK_LANES + lane];
+        for (u32 k = 0; k < 16u; k++) {
+            const u32 y = y0 + k, idx = (gid * PK_ROWS + y) * PK_LANES + lane, l2 = f[k];
+            if (l2 & 0x100u) {
+                render_line(m, y, lat0[idx], lat1[idx], (int)(l2 & 0xFFu) - 1, screen + (size_t)env * PK_SCREEN + y * PK_COLS);
+                lat2[idx] = l2 & ~0x100u;
+            }
         }
     }
 }

@@ -51,7 +51,7 @@
 // diagnostic build only (-DPK_STAMP, tools/stamp_build.py): per-phase wave cycles of the loop,
 // read with s_memtime at points where the loop already waits, summed per wave into A.dbg
 #ifdef PK_STAMP
-#define PK_NSTAMP 5
+#define PK_NSTAMP 12
 #define PK_STAMP_AT(k)                                          \
     do {                                                        \
         const uint64_t t_ = __builtin_amdgcn_s_memtime();       \
@@ -446,11 +446,9 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
                   : action == 4u ? 4u : action == 5u ? 5u : action == 6u ? 7u : action == 7u ? 6u : 0xFFu;
     if (active && btn != 0xFFu) key_event(s, btn, true);
     if (active && A.frames > 0u && A.release_frame == 0u && btn != 0xFFu) key_event(s, btn, false);
+    // (no latch flags to clear for the rendered frame: every consumer of a latched line — K2,
+    // flush_lines, K2's blank-screen path — clears its flag)
     s.render = (A.render_last && frame + 1u == A.frames) ? 1u : 0u;
-    if (s.render) {
-        u32* lat2 = A.lat + 2u * A.lat_stride;
-        for (u32 y = 0; y < PK_ROWS; y++) lat2[(c.gid * PK_ROWS + y) * PK_LANES + c.lane] &= ~0x100u;
-    }
     const uint4* ucv = reinterpret_cast<const uint4*>(lds_uc);
     const u32* romw = reinterpret_cast<const u32*>(lds_rom);
 
@@ -461,11 +459,11 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
     u32 pf = 0, pbytes = 0;
     uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0, p2 = p0;
 #ifdef PK_STAMP
-    uint64_t st_acc[PK_NSTAMP] = {0, 0, 0, 0, 0}, st_prev = __builtin_amdgcn_s_memtime(), st_iter = 0;
+    uint64_t st_acc[PK_NSTAMP] = {}, st_prev = __builtin_amdgcn_s_memtime(), st_iter = 0;
 #endif
     while (frame < A.frames) {
         u32 ev = 0;
-        PK_STAMP_AT(4);
+        PK_STAMP_AT(8);
 #ifdef PK_STAMP
         st_iter++;
 #endif
@@ -493,6 +491,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         u32 bytes = pbytes;
         uint4 e0 = p0, e1 = p1, e2 = p2;
         if (PK_RARE(!pf)) {
+            PK_STAMP_AT(8);
             const bool flds = rom_staged(s, pc) && (pc & 0x3FFFu) < 0x3FFEu;
             const u32 la = sel(flds, rom_lds_index(s, pc), 0u);
             bytes = __builtin_amdgcn_alignbyte(romw[(la >> 2) + 1u], romw[la >> 2], la & 3u);
@@ -528,6 +527,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             e0 = ucv[di * 3u];
             e1 = ucv[di * 3u + 1u];
             e2 = ucv[di * 3u + 2u];
+            PK_STAMP_AT(9);
         }
         icount += sel(exec, 1u, 0u);
         ev |= sel(exec, PK_EV_EXEC | sel((bytes & 0xFFu) == 0xCBu, PK_EV_CB, 0u), 0u) | sel(pf != 0u, PK_EV_F_LDS, 0u)
@@ -576,6 +576,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             om1 = lds_rom[i0 + (u32)sfield(D, PK_DB_ADIR, 2)];  // == om0 for 1-byte reads, masked below
         }
         if (PK_RARE(rd & !rram & !rrom)) {  // rare: IO registers (LY, STAT, joypad, ...), SRAM, unstaged ROM
+            PK_STAMP_AT(0);
             if (!rd2 & (addr0 >= 0xFF00u) & ((addr0 < 0xFF80u) | (addr0 == 0xFFFFu))) {
                 xm = io_read(c, s, addr0);
                 ev |= PK_EV_RD_IO;
@@ -588,6 +589,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
                 xm = pk_read_slow(&A, c.g, c.lane, c.loc, &t, addr0, addr1, rd2 ? 1u : 0u);
                 ev |= PK_EV_RD_ROMG;
             }
+            PK_STAMP_AT(1);
         }
         const u32 m0 = rm0 | om0 | (xm & 0xFFu), m1 = rm1 | sel(rd2, om1, 0u) | (xm >> 8);
         ev |= sel(rd, PK_EV_RD | sel(rd2, PK_EV_RD2, 0u) | sel(rram, PK_EV_RD_RAM, 0u) | sel(rrom, PK_EV_RD_ROMLDS, 0u)
@@ -669,8 +671,11 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             // VRAM / OAM change while rendered lines are pending: rasterise them first (rare)
             // (lines are pending only in the rendered frame: test that first, alone)
             if (PK_RARE(s.npend != 0u)) {
+                PK_STAMP_AT(2);
                 if (vram_or_oam(addr0) | (wr2 & vram_or_oam(addr1))) {
+                    PK_STAMP_AT(11);
                     flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, env, c.gid);
+                    PK_STAMP_AT(10);
                     s.npend = 0;
                     ev |= PK_EV_FLUSH;
                 }
@@ -682,16 +687,17 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
                 hcode_st(c, addr1, wv1);
             }
         }
+        PK_STAMP_AT(2);
         if (PK_RARE(wr & !wram)) {  // rare: IO registers / MBC / SRAM / OAM DMA / IE
             St t = s;
             pk_write_slow(&A, c.g, c.lane, c.loc, env, c.gid, &t, addr0, wv0, addr1, wv1, wr2 ? 1u : 0u);
             s = t;
             ev |= PK_EV_WR_SLOW;
+            PK_STAMP_AT(3);
         }
         ev |= sel(wr, PK_EV_WR | sel(wr2, PK_EV_WR2, 0u) | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
                       | sel(addr0 >= 0xC000u && addr0 < 0xFE00u, PK_EV_WR_WRAM, sel(addr0 >= 0x8000u && addr0 < 0xA000u, PK_EV_WR_VRAM, 0u)), 0u);
 
-        PK_STAMP_AT(1);
         // ---------------- prefetch the next instruction (LDS-staged ROM or the HRAM mirror) ----------------
         {
             const u32 npc = s.pc;
@@ -704,7 +710,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
                 pbytes = lds_hcode[q] | (lds_hcode[q + PK_WG_ENVS] << 8) | (lds_hcode[q + 2u * PK_WG_ENVS] << 16);
             }
             const u32 op = pbytes & 0xFFu;
-            PK_STAMP_AT(2);
+            PK_STAMP_AT(4);
             const u32 di = sel(op == 0xCBu, 256u + ((pbytes >> 8) & 0xFFu), op);
             p0 = ucv[di * 3u];
             p1 = ucv[di * 3u + 1u];
@@ -722,6 +728,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         // so the VBlank event itself is processed below as usual.
         // Both halted-CPU blocks sit behind one `if`: a wave has a halted lane in only a few % of
         // its iterations, so the others skip their ~50 instructions.
+        PK_STAMP_AT(5);
         if (PK_RARE(s.cpu & CPU_HALT)) {
             // a halted CPU fast-forwards to the next LCD event and notices pending interrupts only
             // there, so folded events are observable here: restore the exact event state first
@@ -748,6 +755,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             const int ta = (int)s.target - (int)s.clock;
             const int mm = ta < tb ? ta : tb;
             cycles = (u32)(mm < 0 ? 0 : mm);
+            PK_STAMP_AT(6);
         }
         u32 irq = 0;
         s.divacc = (s.divacc + cycles) & 0xFFFFu;
@@ -820,7 +828,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             s.blank |= s.render;
         }
         s.cpu |= irq << 16;
-        PK_STAMP_AT(3);
+        PK_STAMP_AT(7);
         budget += cycles + 1u;
         ev |= sel(s.frame_done != 0u || budget > 16u * FRAME_CYCLES, PK_EV_FRAME, 0u);
         PK_ITER(env, ev);
@@ -830,10 +838,6 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             frame += 1u;
             if (frame == A.release_frame && btn != 0xFFu) key_event(s, btn, false);
             s.render = (A.render_last && frame + 1u == A.frames) ? 1u : 0u;
-            if (s.render) {
-                u32* lat2 = A.lat + 2u * A.lat_stride;
-                for (u32 y = 0; y < PK_ROWS; y++) lat2[(c.gid * PK_ROWS + y) * PK_LANES + c.lane] &= ~0x100u;
-            }
         }
     }
 

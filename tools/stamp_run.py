@@ -10,8 +10,9 @@ import sys
 HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, HERE)
 STAMP_LIB = os.path.join(HERE, "pokegym_amd", "lib", "libpokegym_amd_stamp.so")
-PHASES = ["front+fetch+read (to the read's wait)", "datapath+control+write", "prefetch fetch (LDS)",
-          "ucode issue+HALT+timer+LCD", "frame end + loop"]
+PHASES = ["front+fetch+read to the read's wait (excl. rare fetch/read)", "rare read block", "datapath+control+fast write",
+          "rare write block", "prefetch (LDS)", "ucode issue", "HALT block", "timer+LCD+latch", "frame end + loop",
+          "rare fetch block", "flush_lines call", "pending-lines check"]
 
 
 def main():
@@ -47,10 +48,10 @@ def main():
         emu.step(a)
     torch.cuda.synchronize()
     L.pk_debug_counters(emu._h, out, 16)
-    it, waves = out[5], max(out[6], 1)
-    res = {"workload": args.workload, "waves": waves, "iterations_per_wave_step": it / waves / args.steps,
+    it, waves = out[12], max(out[13], 1)
+    res = {"workload": args.workload, "waves": waves, "iterations_per_wave_step": it / waves,
            "cycles_per_iteration": {p: round(out[k] / max(it, 1), 1) for k, p in enumerate(PHASES)},
-           "total_per_iteration": round(sum(out[k] for k in range(5)) / max(it, 1), 1)}
+           "total_per_iteration": round(sum(out[k] for k in range(12)) / max(it, 1), 1)}
     print(json.dumps(res))
     emu.close()
 
