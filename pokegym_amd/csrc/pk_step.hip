@@ -703,12 +703,13 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             const u32 npc = s.pc;
             const bool fl = rom_staged(s, npc) && (npc & 0x3FFFu) < 0x3FFEu;
             const u32 la = sel(fl, rom_lds_index(s, npc), 0u);
-            pbytes = __builtin_amdgcn_alignbyte(romw[(la >> 2) + 1u], romw[la >> 2], la & 3u);
+            // staged ROM and the HRAM code mirror are read together, unconditionally (one LDS round
+            // trip; a lane whose pc is not in HRAM reads mirror row 0 and discards it)
             const bool fh = npc - 0xFF80u < 0x7Du;
-            if (fh) {
-                const u32 q = (npc - 0xFF80u) * PK_WG_ENVS + c.loc;
-                pbytes = lds_hcode[q] | (lds_hcode[q + PK_WG_ENVS] << 8) | (lds_hcode[q + 2u * PK_WG_ENVS] << 16);
-            }
+            const u32 q = sel(fh, npc - 0xFF80u, 0u) * PK_WG_ENVS + c.loc;
+            const u32 r0 = romw[la >> 2], r1 = romw[(la >> 2) + 1u];
+            const u32 h0 = lds_hcode[q], h1 = lds_hcode[q + PK_WG_ENVS], h2 = lds_hcode[q + 2u * PK_WG_ENVS];
+            pbytes = sel(fh, h0 | (h1 << 8) | (h2 << 16), __builtin_amdgcn_alignbyte(r1, r0, la & 3u));
             const u32 op = pbytes & 0xFFu;
             PK_STAMP_AT(4);
             const u32 di = sel(op == 0xCBu, 256u + ((pbytes >> 8) & 0xFFu), op);
