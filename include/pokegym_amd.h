@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PK_ABI_VERSION 4
+#define PK_ABI_VERSION 5
 #define PK_STATE_V9_BYTES 142610u
 #define PK_SCREEN_ROWS 144u
 #define PK_SCREEN_COLS 160u
@@ -101,6 +101,15 @@ int pk_reset(pk_handle* h, const uint8_t* env_mask_dev, void* stream);
  *                 (environment.py:1612-1613: terminated = truncated = done). */
 int pk_step(pk_handle* h, const uint8_t* actions_dev, uint8_t* screen_dev, double* rew_dev,
             uint8_t* term_dev, uint8_t* trunc_dev, void* stream);
+
+/* Sub-batch forms (PufferLib batch_size < num_envs, README.md:116-118: 72 envs stepped 24 at a
+ * time): the same step / reset restricted to envs [env0, env0 + count).  env0 and env0 + count
+ * are multiples of 64 (or the end is n).  All arrays stay full-size (device u8/f64[n]); only the
+ * range's elements are read or written, so disjoint ranges may run concurrently on different
+ * streams (each range has its own reset lists). */
+int pk_step_range(pk_handle* h, uint32_t env0, uint32_t count, const uint8_t* actions_dev, double* rew_dev,
+                  uint8_t* term_dev, uint8_t* trunc_dev, void* stream);
+int pk_reset_range(pk_handle* h, uint32_t env0, uint32_t count, const uint8_t* env_mask_dev, void* stream);
 
 /* Rasterise every env's 144 latched scanlines (the per-line SCX/SCY/WX/WY/tile-data latches that
  * pk_create / pk_load_env restore from a v9 savestate, or that the last rendered frame latched)

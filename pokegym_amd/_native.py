@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # PK_LIB selects an alternative in-tree build (A/B kernel experiments); default: lib/libpokegym_amd.so
 LIB_PATH = os.environ.get("PK_LIB") or os.path.join(HERE, "lib", "libpokegym_amd.so")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 PK_F_RENDER = 1
 PK_F_REWARD = 2
 PK_F_RELOAD_ON_RESET = 4
@@ -30,7 +30,7 @@ EXPORTS = ("pk_create", "pk_destroy", "pk_last_error", "pk_abi_version", "pk_res
            "pk_screen_ptr", "pk_num_envs", "pk_peek", "pk_poke", "pk_snapshot", "pk_load_env",
            "pk_last_instr_count", "pk_profile_enable", "pk_profile_read", "pk_obs_ptr", "pk_error_ptr",
            "pk_get_ram", "pk_set_ram", "pk_info_ptr", "pk_info_flag_ptr", "pk_info_stride", "pk_heatmap_ptr", "pk_info_bits_ptr",
-           "pk_snapshot_range", "pk_render_latched")
+           "pk_snapshot_range", "pk_render_latched", "pk_step_range", "pk_reset_range")
 
 
 class PkConfig(ctypes.Structure):
@@ -112,6 +112,8 @@ def bind_v2(L):
     L.pk_get_ram.argtypes = [vp, ctypes.c_uint16, ctypes.c_uint32, vp, vp]
     L.pk_set_ram.argtypes = [vp, ctypes.c_uint16, ctypes.c_uint32, vp, vp]
     L.pk_reset.argtypes = [vp, vp, vp]
+    L.pk_step_range.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp, vp]
+    L.pk_reset_range.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp]
 
 
 def check(rc: int, what: str):

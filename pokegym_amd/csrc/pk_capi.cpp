@@ -23,7 +23,7 @@
 hipError_t pk_launch_step(const PkStepArgs& a, hipStream_t s);
 hipError_t pk_launch_render(const PkStepArgs& a, hipStream_t s);
 hipError_t pk_launch_reset(const PkResetArgs& a, hipStream_t s);
-hipError_t pk_launch_list(const uint8_t* mask, uint32_t n, uint32_t* cnt, uint32_t* ids, hipStream_t s);
+hipError_t pk_launch_list(const uint8_t* mask, uint32_t env0, uint32_t env1, uint32_t* cnt, uint32_t* ids, hipStream_t s);
 hipError_t pk_launch_render_latched(const PkStepArgs& a, hipStream_t s);
 hipError_t pk_launch_gather_env(const uint8_t* mem, uint32_t env, uint8_t* out, hipStream_t s);
 hipError_t pk_launch_gather_range(const uint8_t* mem, uint32_t env0, uint32_t count, uint8_t* out, hipStream_t s);
@@ -222,7 +222,7 @@ void export_v9(const Template& tp, const uint32_t* regs, const uint8_t* mem, con
 struct pk_handle {
     int device = 0;
     uint32_t n = 0, npad = 0, ngroups = 0;
-    uint32_t wave_lanes = 64;  // envs per wave in K1 (see pk_create)
+    uint32_t wave_lanes = 0;   // envs per wave in K1: 0 = by launch size (k1_wave_lanes), else PK_WAVE_LANES
     uint32_t simds = 1024;     // SIMDs of the device (4 per CU)
     uint32_t k1_block = 0;     // K1 workgroup size override (PK_K1_BLOCK), 0 = by geometry
     uint32_t frames = 24, release = 8, flags = 0, max_steps = 20480;
@@ -278,7 +278,7 @@ static int prof_event(pk_handle* h, hipStream_t s) {
 
 extern "C" {
 
-static int template_reset(pk_handle* h, const uint8_t* mask, void* stream);
+static int template_reset(pk_handle* h, const uint8_t* mask, uint32_t env0, uint32_t env1, void* stream);
 
 const char* pk_last_error(void) { return g_err.c_str(); }
 int pk_abi_version(void) { return PK_ABI_VERSION; }
@@ -326,19 +326,12 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     h->npad = (cfg->n_envs + PK_LANES - 1) / PK_LANES * PK_LANES;
     h->ngroups = h->npad / PK_LANES;
     {
-        // K1 wave shape (measured, profiles/r02_sweep_*): two waves per SIMD hide part of each
-        // other's memory and LDS latency, so the envs per wave are the largest of 64/32/16 that
-        // still gives two waves per SIMD (65,536 envs -> 32, 32,768 -> 16); below that 32 (one wave
-        // per SIMD on fewer CUs: spreading 4,096 envs over every CU at 4 per wave measured 2.4x
-        // slower — instruction-issue stalls when every CU runs K1).  PK_WAVE_LANES (a power of
-        // two <= 64) overrides.
+        // K1 wave shape: chosen per launch from the launch's env count (k1_wave_lanes);
+        // PK_WAVE_LANES (a power of two <= 64) fixes it.
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device) != hipSuccess || ncu <= 0) ncu = 256;
         h->simds = 4u * (uint32_t)ncu;
-        h->wave_lanes = 32u;
-        for (uint32_t wl = 64u; wl >= 16u; wl >>= 1) {
-            if (h->npad / wl >= 2u * h->simds) { h->wave_lanes = wl; break; }
-        }
+        h->wave_lanes = 0;
         if (const char* wl = getenv("PK_WAVE_LANES")) {
             int v = atoi(wl);
             if (v < 1 || v > 64 || (v & (v - 1))) { delete h; return fail(-EINVAL, "PK_WAVE_LANES must be a power of two <= 64"); }
@@ -348,7 +341,7 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
         // a multiple of 64 whose envs fit the 256-env HRAM mirror of a workgroup
         if (const char* bl = getenv("PK_K1_BLOCK")) {
             int v = atoi(bl);
-            if (v < 64 || v > 512 || (v % 64) || (uint32_t)(v / 64) * h->wave_lanes > 256u) {
+            if (v < 64 || v > 512 || (v % 64) || (uint32_t)(v / 64) * (h->wave_lanes ? h->wave_lanes : 32u) > 256u) {
                 delete h;
                 return fail(-EINVAL, "PK_K1_BLOCK must be a multiple of 64 in [64, 512] with (block/64)*wave_lanes <= 256");
             }
@@ -394,7 +387,7 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     ALLOC(h->t_lat, 3 * PK_ROWS * 4);
     ALLOC(h->t_screen, PK_SCREEN);
     ALLOC(h->scratch, PK_PHYS + PK_NREGS * 4 + 3 * PK_ROWS * 4 + PK_SCREEN);
-    ALLOC(h->lists, (2 + 2 * (size_t)h->npad) * 4);
+    ALLOC(h->lists, (2 * (size_t)h->ngroups + 2 * (size_t)h->npad) * 4);
 #ifdef PK_STAMP
     ALLOC(h->dbg, 64 * 8);
     (void)hipMemset(h->dbg, 0, 64 * 8);
@@ -459,13 +452,13 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
         pk_destroy(h);
         return fail(-EIO, "device upload failed: %s", hipGetErrorString(e));
     }
-    if ((rc = template_reset(h, nullptr, nullptr))) { pk_destroy(h); return rc; }
+    if ((rc = template_reset(h, nullptr, 0, h->n, nullptr))) { pk_destroy(h); return rc; }
     if (hipDeviceSynchronize() != hipSuccess) { pk_destroy(h); return fail(-EIO, "initial reset failed"); }
     *out = h;
     return 0;
 }
 
-static PkRewardArgs reward_args(pk_handle* h) {
+static PkRewardArgs reward_args(pk_handle* h, uint32_t env0, uint32_t env1) {
     PkRewardArgs r;
     memset(&r, 0, sizeof r);
     r.mem = h->mem; r.regs = h->regs; r.rs = h->rs; r.rsd = h->rsd; r.seen = h->seen; r.mask = h->mask;
@@ -473,44 +466,65 @@ static PkRewardArgs reward_args(pk_handle* h) {
     r.info = h->info; r.info_flag = h->info_flag; r.heat = h->heat; r.info_bits = h->info_bits;
     r.reward_scale = h->reward_scale; r.n = h->n; r.npad = h->npad; r.cap_log2 = h->cap_log2;
     r.max_steps = h->max_steps; r.reload_always = (h->flags & PK_F_RELOAD_ON_RESET) ? 1 : 0;
+    r.env0 = env0; r.env1 = env1;
     return r;
 }
 
-// reload the template state (regs, RAM image, latches, screen) into the masked envs: the envs
-// are listed on the device first, so the reset costs in proportion to the envs it touches
-static int template_reset(pk_handle* h, const uint8_t* mask, void* stream) {
+// reset lists of an env range (env0 % 64 == 0): counters [2 * (env0 / 64)] (reload) and [+1] (obs),
+// ids from env0 in the reload and obs id arrays — disjoint ranges (sub-batches on their own
+// streams) never share a counter or an id slot
+static uint32_t* list_cnt(pk_handle* h, uint32_t env0, int which) { return h->lists + 2u * (env0 / PK_LANES) + which; }
+static uint32_t* list_ids(pk_handle* h, uint32_t env0, int which) {
+    return h->lists + 2u * h->ngroups + (size_t)which * h->npad + env0;
+}
+
+// reload the template state (regs, RAM image, latches, screen) into the masked envs of [env0, env1):
+// the envs are listed on the device first, so the reset costs in proportion to the envs it touches
+static int template_reset(pk_handle* h, const uint8_t* mask, uint32_t env0, uint32_t env1, void* stream) {
     HIPCHK(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
-    HIPCHK(hipMemsetAsync(h->lists, 0, 4, s));
-    HIPCHK(pk_launch_list(mask, h->n, h->lists, h->lists + 2, s));
+    HIPCHK(hipMemsetAsync(list_cnt(h, env0, 0), 0, 4, s));
+    HIPCHK(pk_launch_list(mask, env0, env1, list_cnt(h, env0, 0), list_ids(h, env0, 0), s));
     PkResetArgs a;
     a.mem = h->mem; a.regs = h->regs; a.lat = h->lat; a.screen = h->screen;
     a.tmpl_mem = h->t_mem; a.tmpl_regs = h->t_regs; a.tmpl_lat = h->t_lat; a.tmpl_screen = h->t_screen;
-    a.cnt = h->lists; a.ids = h->lists + 2; a.n = h->n; a.npad = h->npad; a.lat_stride = (uint32_t)h->lat_stride;
+    a.cnt = list_cnt(h, env0, 0); a.ids = list_ids(h, env0, 0); a.n = h->n; a.npad = h->npad;
+    a.lat_stride = (uint32_t)h->lat_stride; a.env0 = env0; a.env1 = env1;
     HIPCHK(pk_launch_reset(a, s));
+    return 0;
+}
+
+static int check_range(pk_handle* h, uint32_t env0, uint32_t count) {
+    if (!h) return fail(-EINVAL, "null handle");
+    if (count == 0 || env0 % PK_LANES || (uint64_t)env0 + count > h->n || ((env0 + count) % PK_LANES && env0 + count != h->n))
+        return fail(-EINVAL, "env range [%u, +%u): start and end must be multiples of 64 (or the end n = %u)", env0, count, h->n);
+    return 0;
+}
+
+int pk_reset_range(pk_handle* h, uint32_t env0, uint32_t count, const uint8_t* mask, void* stream) {
+    int rc;
+    if ((rc = check_range(h, env0, count))) return rc;
+    const uint32_t env1 = env0 + count;
+    if (!(h->flags & PK_F_REWARD)) return template_reset(h, mask, env0, env1, stream);
+    HIPCHK(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    PkRewardArgs r = reward_args(h, env0, env1);
+    r.env_mask = mask;
+    HIPCHK(pk_launch_rreset_pre(r, s));
+    if ((rc = template_reset(h, h->reload, env0, env1, stream))) return rc;
+    HIPCHK(pk_launch_rreset_post(r, s));
+    // the observation of the reset envs only (list of the masked envs)
+    HIPCHK(hipMemsetAsync(list_cnt(h, env0, 1), 0, 4, s));
+    HIPCHK(pk_launch_list(mask, env0, env1, list_cnt(h, env0, 1), list_ids(h, env0, 1), s));
+    r.ocnt = list_cnt(h, env0, 1);
+    r.oids = list_ids(h, env0, 1);
+    HIPCHK(pk_launch_obs(r, s));
     return 0;
 }
 
 int pk_reset(pk_handle* h, const uint8_t* mask, void* stream) {
     if (!h) return fail(-EINVAL, "null handle");
-    if (!(h->flags & PK_F_REWARD)) return template_reset(h, mask, stream);
-    HIPCHK(hipSetDevice(h->device));
-    hipStream_t s = (hipStream_t)stream;
-    PkRewardArgs r = reward_args(h);
-    r.env_mask = mask;
-    HIPCHK(pk_launch_rreset_pre(r, s));
-    int rc = template_reset(h, h->reload, stream);
-    if (rc) return rc;
-    HIPCHK(pk_launch_rreset_post(r, s));
-    // the observation of the reset envs only (list of the masked envs)
-    uint32_t* ocnt = h->lists + 1;
-    uint32_t* oids = h->lists + 2 + h->npad;
-    HIPCHK(hipMemsetAsync(ocnt, 0, 4, s));
-    HIPCHK(pk_launch_list(mask, h->n, ocnt, oids, s));
-    r.ocnt = ocnt;
-    r.oids = oids;
-    HIPCHK(pk_launch_obs(r, s));
-    return 0;
+    return pk_reset_range(h, 0, h->n, mask, stream);
 }
 
 int pk_get_ram(pk_handle* h, uint16_t addr, uint32_t len, uint8_t* dense, void* stream) {
@@ -535,7 +549,18 @@ int pk_set_ram(pk_handle* h, uint16_t addr, uint32_t len, const uint8_t* dense, 
     return 0;
 }
 
-static PkStepArgs step_args(pk_handle* h, const uint8_t* actions) {
+// K1 envs per wave for a launch of `count` envs (measured, profiles/r02_sweep_*): 32 until the
+// launch has two 64-lane waves per SIMD, then 64.  At 65,536 envs two 32-lane waves per SIMD beat
+// one 64-lane wave by ~10 %; at 32,768 one 32-lane wave per SIMD matches two 16-lane ones; below,
+// the launch is latency-bound and more, narrower waves do not help (4,096 envs at 4 per wave on
+// every CU measured 2.4x slower).  PK_WAVE_LANES fixes the shape.
+static uint32_t k1_wave_lanes(const pk_handle* h, uint32_t count) {
+    if (h->wave_lanes) return h->wave_lanes;
+    const uint32_t npad = (count + PK_LANES - 1u) & ~(PK_LANES - 1u);
+    return npad / 64u >= 2u * h->simds ? 64u : 32u;
+}
+
+static PkStepArgs step_args(pk_handle* h, const uint8_t* actions, uint32_t env0, uint32_t env1) {
     PkStepArgs a;
     memset(&a, 0, sizeof a);
     a.mem = h->mem; a.rom = h->rom; a.romw = reinterpret_cast<const uint32_t*>(h->rom); a.regs = h->regs; a.ucode = h->ucode; a.actions = actions;
@@ -544,45 +569,56 @@ static PkStepArgs step_args(pk_handle* h, const uint8_t* actions) {
     a.release_frame = h->release; a.render_last = (h->flags & PK_F_RENDER) ? 1 : 0;
     a.lat_stride = (uint32_t)h->lat_stride;
     a.nslots = h->nslots; a.bank_slot = h->bank_slot; a.slot_bank = h->slot_bank;
-    a.wave_lanes = h->wave_lanes;
+    a.wave_lanes = k1_wave_lanes(h, env1 - env0);
     a.simds = h->simds;
     a.block = h->k1_block;
     a.dbg = h->dbg;
+    a.env0 = env0; a.env1 = env1;
     return a;
 }
 
 int pk_render_latched(pk_handle* h, void* stream) {
     if (!h) return fail(-EINVAL, "null handle");
     HIPCHK(hipSetDevice(h->device));
-    PkStepArgs a = step_args(h, nullptr);
+    PkStepArgs a = step_args(h, nullptr, 0, h->n);
     HIPCHK(pk_launch_render_latched(a, (hipStream_t)stream));
     return 0;
 }
 
-int pk_step(pk_handle* h, const uint8_t* actions, uint8_t* screen_out, double* rew, uint8_t* term,
-            uint8_t* trunc, void* stream) {
-    if (!h) return fail(-EINVAL, "null handle");
+int pk_step_range(pk_handle* h, uint32_t env0, uint32_t count, const uint8_t* actions, double* rew, uint8_t* term,
+                  uint8_t* trunc, void* stream) {
+    int rc;
+    if ((rc = check_range(h, env0, count))) return rc;
     if (!actions) return fail(-EINVAL, "actions_dev is required");
     HIPCHK(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
-    PkStepArgs a = step_args(h, actions);
-    int rc;
+    const uint32_t env1 = env0 + count;
+    PkStepArgs a = step_args(h, actions, env0, env1);
     if (h->prof && (rc = prof_event(h, s))) return rc;
     HIPCHK(pk_launch_step(a, s));
     if (h->prof && (rc = prof_event(h, s))) return rc;
     if (a.render_last) HIPCHK(pk_launch_render(a, s));
     if (h->prof && (rc = prof_event(h, s))) return rc;
     if (h->flags & PK_F_REWARD) {
-        PkRewardArgs r = reward_args(h);
+        PkRewardArgs r = reward_args(h, env0, env1);
         r.actions = actions; r.rew = rew; r.term = term; r.trunc = trunc;
         HIPCHK(pk_launch_reward(r, s));
         HIPCHK(pk_launch_obs(r, s));
     } else if (rew || term || trunc) {
-        HIPCHK(pk_launch_done(h->regs + (size_t)PK_R_TIME * h->npad, h->n, h->max_steps, term, trunc, rew, s));
+        HIPCHK(pk_launch_done(h->regs + (size_t)PK_R_TIME * h->npad + env0, count, h->max_steps, term ? term + env0 : nullptr,
+                              trunc ? trunc + env0 : nullptr, rew ? rew + env0 : nullptr, s));
     }
     if (h->prof && (rc = prof_event(h, s))) return rc;
+    return 0;
+}
+
+int pk_step(pk_handle* h, const uint8_t* actions, uint8_t* screen_out, double* rew, uint8_t* term,
+            uint8_t* trunc, void* stream) {
+    if (!h) return fail(-EINVAL, "null handle");
+    int rc = pk_step_range(h, 0, h->n, actions, rew, term, trunc, stream);
+    if (rc) return rc;
     if (screen_out)
-        HIPCHK(hipMemcpyAsync(screen_out, h->screen, (size_t)h->n * PK_SCREEN, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(screen_out, h->screen, (size_t)h->n * PK_SCREEN, hipMemcpyDeviceToDevice, (hipStream_t)stream));
     return 0;
 }
 

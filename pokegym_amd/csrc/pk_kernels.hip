@@ -19,10 +19,10 @@
 // lane = env: the 64 lanes read the same VRAM offsets of their interleaved images (coalesced).
 __global__ void __launch_bounds__(64) pk_render_kernel(PkStepArgs A) {
     const u32 y = blockIdx.x % PK_ROWS;
-    const u32 gid = blockIdx.x / PK_ROWS;
+    const u32 gid = A.env0 / PK_LANES + blockIdx.x / PK_ROWS;
     const u32 lane = threadIdx.x;
     const u32 env = gid * PK_LANES + lane;
-    if (env >= A.n) return;
+    if (env >= A.env1) return;
     const u32 rf = A.regs[PK_R_RFLAGS * A.npad + env];
     u8* out = A.screen + (size_t)env * PK_SCREEN + y * PK_COLS;
     const u32 idx = (gid * PK_ROWS + y) * PK_LANES + lane;
@@ -67,9 +67,9 @@ __global__ void __launch_bounds__(256) pk_arm_latches_kernel(PkStepArgs A) {
 // The reset kernels work on a device-built list of the envs to reset (pk_list_kernel: ids of the
 // masked envs, count in device memory), so a step where few or no envs finish costs a few
 // near-empty launches instead of a scan of every env's 49.7 KB image — and no host sync.
-__global__ void __launch_bounds__(256) pk_list_kernel(const u8* mask, u32 n, u32* cnt, u32* ids) {
-    const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n || (mask && !mask[e])) return;
+__global__ void __launch_bounds__(256) pk_list_kernel(const u8* mask, u32 env0, u32 env1, u32* cnt, u32* ids) {
+    const u32 e = env0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= env1 || (mask && !mask[e])) return;
     ids[atomicAdd(cnt, 1u)] = e;
 }
 
@@ -128,20 +128,20 @@ __global__ void pk_scatter_env_kernel(u8* mem, u32 env, const u8* in) {
 // ---------------------------------------------------------------------------------------------
 // host-side launchers (called by the C ABI in pk_capi.cpp)
 hipError_t pk_launch_render(const PkStepArgs& a, hipStream_t s) {
-    const u32 grid = (a.npad / PK_LANES) * PK_ROWS;
+    const u32 grid = ((a.env1 - a.env0 + PK_LANES - 1u) / PK_LANES) * PK_ROWS;
     hipLaunchKernelGGL(pk_render_kernel, dim3(grid), dim3(PK_LANES), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t pk_launch_render_latched(const PkStepArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(pk_arm_latches_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(pk_arm_latches_kernel, dim3((a.env1 + 255) / 256), dim3(256), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return pk_launch_render(a, s);
 }
 
-hipError_t pk_launch_list(const u8* mask, u32 n, u32* cnt, u32* ids, hipStream_t s) {
-    hipLaunchKernelGGL(pk_list_kernel, dim3((n + 255) / 256), dim3(256), 0, s, mask, n, cnt, ids);
+hipError_t pk_launch_list(const u8* mask, u32 env0, u32 env1, u32* cnt, u32* ids, hipStream_t s) {
+    hipLaunchKernelGGL(pk_list_kernel, dim3((env1 - env0 + 255) / 256), dim3(256), 0, s, mask, env0, env1, cnt, ids);
     return hipGetLastError();
 }
 
@@ -150,7 +150,7 @@ hipError_t pk_launch_reset(const PkResetArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(pk_reset_mem_kernel, dim3(4096), dim3(256), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(pk_reset_regs_kernel, dim3((a.npad + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(pk_reset_regs_kernel, dim3((a.env1 - a.env0 + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -87,6 +87,7 @@ struct PkStepArgs {
     uint32_t simds;           // SIMDs of the device: K1 uses 256-thread workgroups while waves <= simds
     uint32_t block;           // K1 workgroup size override (0 = by geometry; PK_K1_BLOCK, tests)
     unsigned long long* dbg;  // diagnostic counters (-DPK_STAMP builds only), else null
+    uint32_t env0, env1;      // env range of this launch: [env0, env1), env0 % 64 == 0 (sub-batches)
 };
 
 struct PkResetArgs {
@@ -101,4 +102,5 @@ struct PkResetArgs {
     const uint32_t* cnt;         // envs to reset: count (device memory) ...
     const uint32_t* ids;         // ... and their ids (pk_list_kernel)
     uint32_t n, npad, lat_stride;
+    uint32_t env0, env1;         // env range the list was built over
 };

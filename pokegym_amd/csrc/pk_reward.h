@@ -107,4 +107,5 @@ struct PkRewardArgs {
     uint32_t cap_log2;        // seen table capacity = 1 << cap_log2
     uint32_t max_steps;
     uint32_t reload_always;   // PK_F_RELOAD_ON_RESET
+    uint32_t env0, env1;      // env range of this launch (sub-batches); arrays stay full-size [n]
 };

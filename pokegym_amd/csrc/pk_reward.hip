@@ -225,8 +225,8 @@ __device__ __constant__ u32 k_opp_level[6] = {0xD8C5, 0xD8F1, 0xD91D, 0xD949, 0x
 // ---------------------------------------------------------------------------------------------
 // K4: one env-step of the reward stack
 __global__ void __launch_bounds__(256) pk_reward_kernel(PkRewardArgs A) {
-    const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= A.n) return;
+    const u32 e = A.env0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= A.env1) return;
     const u32 np = A.npad;
     u32* rs = A.rs;
     double* rsd = A.rsd;
@@ -616,8 +616,8 @@ __global__ void __launch_bounds__(256) pk_reward_kernel(PkRewardArgs A) {
 // K5r (before the template reload): get_base_event_flags' D778 write (:1137-1138) and the
 // reload decision (reload only on the first reset, :1241-1242, unless PK_F_RELOAD_ON_RESET)
 __global__ void __launch_bounds__(256) pk_rreset_pre_kernel(PkRewardArgs A) {
-    const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= A.n) return;
+    const u32 e = A.env0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= A.env1) return;
     const bool sel = !A.env_mask || A.env_mask[e];
     u8 rl = 0;
     if (sel) {
@@ -636,8 +636,8 @@ __global__ void __launch_bounds__(256) pk_rreset_pre_kernel(PkRewardArgs A) {
 
 // K5r (after the reload): the per-episode attributes of reset() and its three update_* calls
 __global__ void __launch_bounds__(256) pk_rreset_post_kernel(PkRewardArgs A) {
-    const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= A.n) return;
+    const u32 e = A.env0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= A.env1) return;
     if (A.env_mask && !A.env_mask[e]) return;
     const u32 np = A.npad;
     u32* rs = A.rs;
@@ -687,13 +687,13 @@ __global__ void __launch_bounds__(256) pk_rreset_post_kernel(PkRewardArgs A) {
 // One thread = 4 consecutive pixels (one 16-byte store); grid-stride over (env, row, quad).
 // With a list (A.ocnt/A.oids: the envs a reset touched) only those envs are rebuilt.
 __global__ void __launch_bounds__(256) pk_obs_kernel(PkRewardArgs A) {
-    const u32 cnt = A.ocnt ? *A.ocnt : A.n;
+    const u32 cnt = A.ocnt ? *A.ocnt : A.env1 - A.env0;
     const size_t total = (size_t)cnt * PK_OBS_H * (PK_OBS_W / 4u);
     for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
         const u32 q = (u32)(t % (PK_OBS_W / 4u));
         const u32 y = (u32)((t / (PK_OBS_W / 4u)) % PK_OBS_H);
         const u32 k = (u32)(t / ((size_t)PK_OBS_H * (PK_OBS_W / 4u)));
-        const u32 e = A.oids ? A.oids[k] : k;
+        const u32 e = A.oids ? A.oids[k] : A.env0 + k;
         const u8* g = A.mem + (size_t)(e / PK_LANES) * PK_GROUP_STRIDE + (e % PK_LANES);
         const int r = g[(size_t)(PK_P_WRAM + 0x1361u) * PK_LANES];
         const int c = g[(size_t)(PK_P_WRAM + 0x1362u) * PK_LANES];
@@ -734,22 +734,22 @@ __global__ void __launch_bounds__(256) pk_ram_copy_kernel(uint8_t* mem, uint8_t*
 
 // ---------------------------------------------------------------------------------------------
 hipError_t pk_launch_reward(const PkRewardArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(pk_reward_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(pk_reward_kernel, dim3((a.env1 - a.env0 + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t pk_launch_rreset_pre(const PkRewardArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(pk_rreset_pre_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(pk_rreset_pre_kernel, dim3((a.env1 - a.env0 + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t pk_launch_rreset_post(const PkRewardArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(pk_rreset_post_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(pk_rreset_post_kernel, dim3((a.env1 - a.env0 + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t pk_launch_obs(const PkRewardArgs& a, hipStream_t s) {
-    const size_t total = (size_t)a.n * PK_OBS_H * (PK_OBS_W / 4u);
+    const size_t total = (size_t)(a.env1 - a.env0) * PK_OBS_H * (PK_OBS_W / 4u);
     const u32 grid = (u32)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
     hipLaunchKernelGGL(pk_obs_kernel, dim3(grid), dim3(256), 0, s, a);
     return hipGetLastError();

@@ -399,8 +399,8 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
     const u32 tid = blk * blockDim.x + threadIdx.x;
     const u32 wl = tid & (PK_LANES - 1u);
     if (wl >= A.wave_lanes) return;
-    const u32 env = (tid >> 6) * A.wave_lanes + wl;
-    if (env >= A.npad) return;
+    const u32 env = A.env0 + (tid >> 6) * A.wave_lanes + wl;   // env0: first env of the sub-batch
+    if (env >= ((A.env1 + PK_LANES - 1u) & ~(PK_LANES - 1u))) return;
     Ctx c;
     c.A = &A;
     c.lane = env & (PK_LANES - 1u);
@@ -437,9 +437,9 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
     s.frame_done = 0;
     u32 icount = 0;
 
-    const bool active = env < A.n;
+    const bool active = env < A.env1;
     u32 frame = active ? 0u : A.frames;
-    const u32 action = active ? A.actions[env] : 8u;
+    const u32 action = active ? A.actions[env] : 8u;   // actions: full-size [n] array
     // pyboy_binding.py:7-40 ACTIONS: Down Left Right Up A B Start Select -> interaction buttons
     // (0 Right 1 Left 2 Up 3 Down 4 A 5 B 6 Select 7 Start); 8+ = no button (extension)
     const u32 btn = action == 0u ? 3u : action == 1u ? 1u : action == 2u ? 0u : action == 3u ? 2u
@@ -874,7 +874,8 @@ hipError_t pk_launch_step(const PkStepArgs& a, hipStream_t s) {
     // one wave per SIMD while the waves fit, else 512-thread workgroups put two waves on each SIMD
     // of a CU (the ~115 KB of LDS staging allows one workgroup per CU)
     const u32 wl = a.wave_lanes;
-    const u32 threads = a.npad * (PK_LANES / wl);
+    const u32 span = ((a.env1 + PK_LANES - 1u) & ~(PK_LANES - 1u)) - a.env0;
+    const u32 threads = span * (PK_LANES / wl);
     const u32 wide = 256u * PK_LANES / wl < PK_K1_MAX_THREADS ? 256u * PK_LANES / wl : PK_K1_MAX_THREADS;
     const u32 block = a.block ? a.block : (threads / PK_LANES <= a.simds ? 256u : wide);
     const u32 grid = (threads + block - 1) / block;

@@ -30,34 +30,38 @@ def env_rank() -> tuple[int, int, int]:
 
 
 class EpisodeStats:
-    """Device-resident per-env episode accumulators + a 5-float64 summary all-reduced over ranks."""
+    """Device-resident per-env episode accumulators + a 5-float64 summary all-reduced over ranks.
+    With sub-batches (VecEnv batch_size < num_envs, each stepped on its own stream) every
+    sub-batch accumulates into its own summary row, so concurrent updates never share a tensor."""
 
-    def __init__(self, n: int, device):
+    def __init__(self, n: int, device, nbatches: int = 1):
         self.device = torch.device(device)
         self.ep_return = torch.zeros(n, dtype=torch.float64, device=self.device)
         self.ep_length = torch.zeros(n, dtype=torch.float64, device=self.device)
-        self.summary = torch.zeros(len(STAT_FIELDS), dtype=torch.float64, device=self.device)
+        self.summary = torch.zeros((nbatches, len(STAT_FIELDS)), dtype=torch.float64, device=self.device)
 
-    def update(self, rewards: torch.Tensor, done: torch.Tensor):
-        """Accumulate one step; finished episodes move into the summary (no host sync)."""
+    def update(self, rewards: torch.Tensor, done: torch.Tensor, batch: int = 0, envs: slice = slice(None)):
+        """Accumulate one step of the envs `envs` (rewards/done cover exactly those envs);
+        finished episodes move into the summary row `batch` (no host sync)."""
         d = done.to(torch.float64)
-        self.ep_return.add_(rewards.to(torch.float64))
-        self.ep_length.add_(1.0)
-        s = self.summary
-        s[0] += (self.ep_return * d).sum()
+        ret, length = self.ep_return[envs], self.ep_length[envs]
+        ret.add_(rewards.to(torch.float64))
+        length.add_(1.0)
+        s = self.summary[batch]
+        s[0] += (ret * d).sum()
         s[1] += d.sum()
-        s[2] += (self.ep_length * d).sum()
+        s[2] += (length * d).sum()
         s[3] += rewards.to(torch.float64).sum()
         s[4] += float(rewards.numel())
         keep = 1.0 - d
-        self.ep_return.mul_(keep)
-        self.ep_length.mul_(keep)
+        ret.mul_(keep)
+        length.mul_(keep)
 
     def allreduce(self, group=None, reset: bool = True) -> dict:
         """Sum the summaries of all ranks (RCCL over xGMI when the tensors live on GPUs).  With
         reset (the default, like InfoStats) the summary restarts, so each call covers one logging
         interval; per-env episodes in progress keep accumulating."""
-        out = self.summary.clone()
+        out = self.summary.sum(dim=0)
         if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
             dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
         if reset:
@@ -77,20 +81,22 @@ class InfoStats:
     one, plus their count; all-reduced and averaged per logging interval, like PufferLib's mean over
     the info dicts its envs returned."""
 
-    def __init__(self, device):
+    def __init__(self, device, nbatches: int = 1):
         from .info import NFIELDS
         self.device = torch.device(device)
-        self.sum = torch.zeros(NFIELDS + 1, dtype=torch.float64, device=self.device)   # last = count
+        # one row per sub-batch (concurrent streams); last column = count
+        self.sum = torch.zeros((nbatches, NFIELDS + 1), dtype=torch.float64, device=self.device)
 
-    def update(self, info: torch.Tensor, flag: torch.Tensor):
-        """info: f64 (NFIELDS, n) view, flag: (n,) 0/1 — one GEMV, no host sync."""
+    def update(self, info: torch.Tensor, flag: torch.Tensor, batch: int = 0):
+        """info: f64 (NFIELDS, m) view, flag: (m,) 0/1 of the same envs — one GEMV, no host sync."""
         f = flag.to(torch.float64)
-        self.sum[:-1] += torch.mv(info, f)
-        self.sum[-1] += f.sum()
+        row = self.sum[batch]
+        row[:-1] += torch.mv(info, f)
+        row[-1] += f.sum()
 
     def allreduce(self, group=None, reset: bool = True) -> dict:
         from .info import REWARD_FIELDS, STATS_FIELDS
-        out = self.sum.clone()
+        out = self.sum.sum(dim=0)
         if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
             dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
         if reset:

@@ -94,6 +94,7 @@ class BatchedEmulator:
         self.rewards = torch.zeros(self.n, dtype=torch.float64, device=self.device)
         self.terminals = torch.zeros(self.n, dtype=torch.uint8, device=self.device)
         self.truncations = torch.zeros(self.n, dtype=torch.uint8, device=self.device)
+        self.actions = torch.full((self.n,), 8, dtype=torch.uint8, device=self.device)  # sub-batch staging
 
     # -- stream helpers -----------------------------------------------------------------
     def _stream(self):
@@ -111,6 +112,32 @@ class BatchedEmulator:
                               ctypes.c_void_p(self.terminals.data_ptr()),
                               ctypes.c_void_p(self.truncations.data_ptr()), self._stream()), "pk_step")
         return (self.obs if self.reward else self.screen), self.rewards, self.terminals, self.truncations
+
+    def step_range(self, env0: int, actions: torch.Tensor):
+        """One env-step of the sub-batch [env0, env0 + len(actions)) only (pk_step_range), on the
+        current stream: env0 and the end are multiples of 64 (or the end is n).  Returns views of
+        the sub-batch's (obs, rewards, terminals, truncations)."""
+        count = actions.numel()
+        sl = slice(env0, env0 + count)
+        self.actions[sl].copy_(actions.reshape(-1))
+        check(self._L.pk_step_range(self._h, env0, count, ctypes.c_void_p(self.actions.data_ptr()),
+                                    ctypes.c_void_p(self.rewards.data_ptr()), ctypes.c_void_p(self.terminals.data_ptr()),
+                                    ctypes.c_void_p(self.truncations.data_ptr()), self._stream()), "pk_step_range")
+        obs = self.obs if self.reward else self.screen
+        return obs[sl], self.rewards[sl], self.terminals[sl], self.truncations[sl]
+
+    def reset_range(self, env0: int, count: int, mask: torch.Tensor | None = None):
+        """Reset the envs of [env0, env0 + count) — all of them, or those with mask[e] != 0 where
+        mask is a FULL-size (n) device u8 tensor (e.g. `terminals`; only the range is read) —
+        pk_reset_range on the current stream."""
+        mp = None
+        if mask is not None:
+            if mask.dtype != torch.uint8 or mask.device != self.device or mask.numel() != self.n or not mask.is_contiguous():
+                raise ValueError("reset_range mask must be a contiguous uint8 tensor of n_envs elements on the device")
+            mp = ctypes.c_void_p(mask.data_ptr())
+        check(self._L.pk_reset_range(self._h, env0, count, mp, self._stream()), "pk_reset_range")
+        obs = self.obs if self.reward else self.screen
+        return obs[env0:env0 + count]
 
     def reset(self, mask: torch.Tensor | None = None):
         """Reset all envs (mask None) or those with mask[e] != 0 (device tensor).  Returns the obs."""

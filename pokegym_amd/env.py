@@ -108,12 +108,21 @@ class Environment:
 
 
 class VecEnv:
-    """N envs on one GPU with PufferLib-style batch semantics (device tensors in and out)."""
+    """N envs on one GPU with PufferLib-style batch semantics (device tensors in and out).
+
+    batch_size < num_envs splits the envs into num_envs / batch_size sub-batches (the reference
+    trains 72 envs 24 at a time, README.md:116-118): recv() returns the next sub-batch whose step
+    has finished, send(actions) steps the sub-batch the last recv() returned on its own HIP stream
+    (pk_step_range) and returns immediately, so the policy works on one sub-batch while the GPU
+    steps the others.  batch_size must divide num_envs and be a multiple of 64.  step(actions)
+    steps all envs at once (batch_size == num_envs).  Sub-batches overlap on the GPU while the HIP
+    runtime has a hardware queue per stream (GPU_MAX_HW_QUEUES, 4 by default: the default stream plus
+    up to 3 sub-batches; beyond that streams share queues and their launches serialise)."""
 
     def __init__(self, num_envs: int, rom_path=None, state_path=None, rom: bytes | None = None, state: bytes | None = None,
                  device: int | None = None, max_episode_steps: int = 20480, reward_scale: float = 4.0,
                  reload_on_reset: bool = False, env_offset: int = 0, log_interval: int = 128, emulator=None,
-                 heatmap: bool = False, reward: bool = True, power_on: bool = False):
+                 heatmap: bool = False, reward: bool = True, power_on: bool = False, batch_size: int | None = None):
         """reward=False: the screen-obs env of configs[3] — obs is the (144, 160) u8 screen, rewards are
         0 and episodes end at max_episode_steps.  power_on=True starts (and resets) every env from
         the cartridge's power-on state instead of a savestate."""
@@ -130,13 +139,18 @@ class VecEnv:
         self.emu = emulator
         self.device = emulator.device
         self.num_envs = self.num_agents = num_envs
+        self.batch_size = batch_size or num_envs
+        if num_envs % self.batch_size or (self.batch_size != num_envs and self.batch_size % 64):
+            raise ValueError("batch_size must divide num_envs and be a multiple of 64")
+        self.num_batches = num_envs // self.batch_size
         self.single_observation_space = (spaces.observation_space() if getattr(emulator, "reward", True)
                                          else spaces.screen_space())
         self.single_action_space = spaces.action_space()
         self.env_ids = torch.arange(env_offset, env_offset + num_envs, device=self.device)
         self.masks = torch.ones(num_envs, dtype=torch.bool, device=self.device)
-        self.stats = EpisodeStats(num_envs, self.device)
-        self.info_stats = InfoStats(self.device) if getattr(emulator, "info", None) is not None else None
+        self.stats = EpisodeStats(num_envs, self.device, self.num_batches)
+        self.info_stats = (InfoStats(self.device, self.num_batches) if getattr(emulator, "info", None) is not None
+                           else None)
         self.log_interval = log_interval
         self.t = 0
         self._pending = None
@@ -145,6 +159,16 @@ class VecEnv:
         # the next logging interval — an exception between two checks is not lost
         errs = getattr(emulator, "errors", None)
         self.sticky_errors = torch.zeros_like(errs) if errs is not None else None
+        # sub-batch pipeline (batch_size < num_envs): one stream + completion event per sub-batch,
+        # FIFO of finished ones
+        self._streams = [torch.cuda.Stream(self.device) for _ in range(self.num_batches)] if self.num_batches > 1 else []
+        self._events = [torch.cuda.Event() for _ in range(self.num_batches)] if self.num_batches > 1 else []
+        self._ready: list[int] = []
+        self._current: int | None = None
+        self._batch_steps = 0
+
+    def _range(self, b: int) -> slice:
+        return slice(b * self.batch_size, (b + 1) * self.batch_size)
 
     def reset(self, seed=None):
         obs = self.emu.reset()
@@ -166,28 +190,54 @@ class VecEnv:
             raise ERR_EXCEPTIONS.get(code, RuntimeError)(
                 f"env {e}: reference reward stack raises here (PK_ERR {code}); {bad.numel()} env(s) failed")
 
-    def step(self, actions):
-        if isinstance(actions, np.ndarray):
-            actions = torch.from_numpy(actions)
-        a = actions.to(device=self.device, dtype=torch.uint8).contiguous()
-        obs, rew, term, trunc = self.emu.step(a)
+    def _step_range(self, b: int, actions: torch.Tensor):
+        """Step sub-batch b (envs _range(b)) on the current stream, then book-keep and auto-reset."""
+        sl = self._range(b)
+        if self.num_batches == 1:
+            obs, rew, term, trunc = self.emu.step(actions)
+        else:
+            obs, rew, term, trunc = self.emu.step_range(sl.start, actions)
+        self.stats.update(rew, term, batch=b, envs=sl)
+        if self.info_stats is not None:
+            self.info_stats.update(self.emu.info[:, sl], self.emu.info_flag[sl], batch=b)
+        if self.sticky_errors is not None:
+            se = self.sticky_errors[sl]
+            torch.where(se != 0, se, self.emu.errors[sl], out=se)
         rewards = rew.clone()
         terminals = term.to(torch.bool)
         truncations = trunc.to(torch.bool)
-        self.stats.update(rewards, term)
-        if self.info_stats is not None:
-            self.info_stats.update(self.emu.info, self.emu.info_flag)
-        if self.sticky_errors is not None:
-            torch.where(self.sticky_errors != 0, self.sticky_errors, self.emu.errors, out=self.sticky_errors)
-        self.emu.reset(term)  # auto-reset finished envs (no host sync)
-        self.t += 1
+        # auto-reset the finished envs (no host sync); their obs is the first obs of the next episode
+        if self.num_batches == 1:
+            self.emu.reset(term)
+        else:
+            self.emu.reset_range(sl.start, self.batch_size, self.emu.terminals)
+        return obs, rewards, terminals, truncations
+
+    def _log(self):
         infos = []
-        if self.log_interval and self.t % self.log_interval == 0:
+        if self.log_interval and self._batch_steps % (self.log_interval * self.num_batches) == 0:
             self.raise_if_failed()
             infos = [self.stats.allreduce()]
             if self.info_stats is not None:
                 infos[0].update(self.info_stats.allreduce())
-        return obs, rewards, terminals, truncations, infos
+        return infos
+
+    def step(self, actions):
+        """Step every env (all sub-batches) with actions of shape (num_envs,)."""
+        if isinstance(actions, np.ndarray):
+            actions = torch.from_numpy(actions)
+        a = actions.to(device=self.device, dtype=torch.uint8).contiguous()
+        if self.num_batches == 1:
+            obs, rewards, terminals, truncations = self._step_range(0, a)
+        else:
+            outs = [self._step_range(b, a[self._range(b)]) for b in range(self.num_batches)]
+            obs = self.emu.obs if self.emu.reward else self.emu.screen
+            rewards = torch.cat([o[1] for o in outs])
+            terminals = torch.cat([o[2] for o in outs])
+            truncations = torch.cat([o[3] for o in outs])
+        self.t += 1
+        self._batch_steps += self.num_batches
+        return obs, rewards, terminals, truncations, self._log()
 
     def save_state(self, env: int) -> bytes:
         """PyBoy v9 savestate of one env (pk_snapshot; environment.py:208-213 per env)."""
@@ -208,21 +258,77 @@ class VecEnv:
             dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
         return out
 
-    # PufferLib async API
+    # PufferLib async API: async_reset, then repeatedly recv() -> policy -> send(actions)
     def async_reset(self, seed=None):
         obs, infos = self.reset(seed)
-        z = torch.zeros(self.num_envs, device=self.device)
+        if self.num_batches == 1:   # one batch: send() steps synchronously on the current stream
+            z = torch.zeros(self.num_envs, device=self.device)
+            f = torch.zeros(self.num_envs, dtype=torch.bool, device=self.device)
+            self._pending = (obs, z, f, f, infos)
+            return
+        cur = torch.cuda.current_stream(self.device)
+        z = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
         f = torch.zeros(self.num_envs, dtype=torch.bool, device=self.device)
-        self._pending = (obs, z, f, f, infos)
-
-    def send(self, actions):
-        self._pending = self.step(actions)
+        self._pending = [(z[self._range(b)], f[self._range(b)], f[self._range(b)]) for b in range(self.num_batches)]
+        for b in range(self.num_batches):
+            self._events[b].record(cur)
+        self._ready = list(range(self.num_batches))
+        self._current = None
 
     def recv(self):
-        obs, rew, term, trunc, infos = self._pending
-        return obs, rew, term, trunc, infos, self.env_ids, self.masks
+        """The next finished sub-batch: (obs, rewards, terminals, truncations, infos, env_ids, masks),
+        device tensors over its batch_size envs; the current stream waits for its step (no host sync)."""
+        if self.num_batches == 1:
+            obs, rew, term, trunc, infos = self._pending
+            return obs, rew, term, trunc, infos, self.env_ids, self.masks
+        if self._current is not None:
+            raise RuntimeError("recv() called twice without send()")
+        if not self._ready:
+            raise RuntimeError("recv() before async_reset()")
+        b = self._ready.pop(0)
+        torch.cuda.current_stream(self.device).wait_event(self._events[b])
+        self._current = b
+        sl = self._range(b)
+        rew, term, trunc = self._pending[b]
+        obs = self.emu.obs if self.emu.reward else self.emu.screen
+        infos, self._pending_infos = getattr(self, "_pending_infos", []), []
+        return obs[sl], rew, term, trunc, infos, self.env_ids[sl], self.masks[sl]
+
+    def current_envs(self) -> slice:
+        """Local env range of the sub-batch the last recv() returned (host-side, no sync)."""
+        return self._range(self._current) if self.num_batches > 1 else slice(0, self.num_envs)
+
+    def send(self, actions):
+        """Step the sub-batch the last recv() returned, with actions (batch_size,), on its own stream."""
+        if self.num_batches == 1:
+            self._pending = self.step(actions)
+            return
+        b = self._current
+        if b is None:
+            raise RuntimeError("send() without a preceding recv()")
+        if isinstance(actions, np.ndarray):
+            actions = torch.from_numpy(actions)
+        cur = torch.cuda.current_stream(self.device)
+        a = actions.to(device=self.device, dtype=torch.uint8).contiguous()
+        st = self._streams[b]
+        st.wait_stream(cur)                       # the policy's actions (and its reads of obs)
+        with torch.cuda.stream(st):
+            a.record_stream(st)
+            _, rew, term, trunc = self._step_range(b, a)
+            self._events[b].record(st)
+        self._pending[b] = (rew, term, trunc)
+        self._batch_steps += 1
+        if self._batch_steps % self.num_batches == 0:
+            self.t += 1
+        logged = self._log()
+        if logged:
+            self._pending_infos = logged
+        self._ready.append(b)
+        self._current = None
 
     def close(self):
+        if self._streams:
+            torch.cuda.synchronize(self.device)
         self.emu.close()
 
 
