@@ -111,6 +111,12 @@ int pk_step_range(pk_handle* h, uint32_t env0, uint32_t count, const uint8_t* ac
                   uint8_t* term_dev, uint8_t* trunc_dev, void* stream);
 int pk_reset_range(pk_handle* h, uint32_t env0, uint32_t count, const uint8_t* env_mask_dev, void* stream);
 
+/* Environment.reset(max_episode_steps, reward_scale) (environment.py:1233, :1258-1259): set the
+ * episode length and reward scale for the following steps (all envs of the handle).  Synchronous
+ * when the seen-coordinate set must grow for a longer episode (it restarts empty then); call it
+ * before the reset it belongs to. */
+int pk_set_episode_params(pk_handle* h, uint32_t max_episode_steps, double reward_scale);
+
 /* Rasterise every env's 144 latched scanlines (the per-line SCX/SCY/WX/WY/tile-data latches that
  * pk_create / pk_load_env restore from a v9 savestate, or that the last rendered frame latched)
  * into the screen with K2, the HIP renderer of pk_step — PyBoy's renderer.scanline over a loaded

@@ -30,7 +30,8 @@ EXPORTS = ("pk_create", "pk_destroy", "pk_last_error", "pk_abi_version", "pk_res
            "pk_screen_ptr", "pk_num_envs", "pk_peek", "pk_poke", "pk_snapshot", "pk_load_env",
            "pk_last_instr_count", "pk_profile_enable", "pk_profile_read", "pk_obs_ptr", "pk_error_ptr",
            "pk_get_ram", "pk_set_ram", "pk_info_ptr", "pk_info_flag_ptr", "pk_info_stride", "pk_heatmap_ptr", "pk_info_bits_ptr",
-           "pk_snapshot_range", "pk_render_latched", "pk_step_range", "pk_reset_range")
+           "pk_snapshot_range", "pk_render_latched", "pk_step_range", "pk_reset_range",
+           "pk_set_episode_params")
 
 
 class PkConfig(ctypes.Structure):
@@ -114,6 +115,7 @@ def bind_v2(L):
     L.pk_reset.argtypes = [vp, vp, vp]
     L.pk_step_range.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp, vp]
     L.pk_reset_range.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp]
+    L.pk_set_episode_params.argtypes = [vp, ctypes.c_uint32, ctypes.c_double]
 
 
 def check(rc: int, what: str):

@@ -847,6 +847,32 @@ int pk_profile_read(pk_handle* h, double* emu_ms, double* render_ms, double* rew
     return 0;
 }
 
+// Environment.reset(max_episode_steps, reward_scale) (environment.py:1233, :1258-1259): the episode
+// length and reward scale of the following steps.  The seen-coordinate set grows (and restarts
+// empty) when the new episode length needs more capacity; call it before the reset it belongs to.
+int pk_set_episode_params(pk_handle* h, uint32_t max_episode_steps, double reward_scale) {
+    if (!h) return fail(-EINVAL, "null handle");
+    if (max_episode_steps == 0) return fail(-EINVAL, "max_episode_steps must be > 0");
+    HIPCHK(hipSetDevice(h->device));
+    if (h->flags & PK_F_REWARD) {
+        uint32_t need = 10;
+        while ((1ull << need) * 3 < ((uint64_t)max_episode_steps + 2) * 4) need++;
+        if (need > h->cap_log2) {
+            HIPCHK(hipDeviceSynchronize());
+            uint32_t* seen = nullptr;
+            const size_t bytes = (size_t)h->npad * (1ull << need) * 4;
+            if (hipMalloc((void**)&seen, bytes) != hipSuccess) return fail(-ENOMEM, "hipMalloc(%zu) for the seen set", bytes);
+            if (hipMemset(seen, 0, bytes) != hipSuccess) { (void)hipFree(seen); return fail(-EIO, "hipMemset failed"); }
+            (void)hipFree(h->seen);
+            h->seen = seen;
+            h->cap_log2 = need;
+        }
+    }
+    h->max_steps = max_episode_steps;
+    h->reward_scale = reward_scale;
+    return 0;
+}
+
 // diagnostic: the K1 phase-cycle counters of a -DPK_STAMP build (zeros otherwise), then reset
 int pk_debug_counters(pk_handle* h, uint64_t* out, uint32_t n) {
     if (!h || !out) return fail(-EINVAL, "null argument");

@@ -67,6 +67,7 @@ class BatchedEmulator:
         self._h = h
         self.render = render
         self.reward = reward
+        self.max_episode_steps, self.reward_scale = int(max_episode_steps), float(reward_scale)
         ptr = self._L.pk_screen_ptr(self._h)
         self.screen = torch.as_tensor(_CudaArray(ptr, (self.n, ROWS, COLS), "|u1"), device=self.device)
         self.obs = None
@@ -147,6 +148,12 @@ class BatchedEmulator:
             mp = ctypes.c_void_p(mask.data_ptr())
         check(self._L.pk_reset(self._h, mp, self._stream()), "pk_reset")
         return self.obs if self.reward else self.screen
+
+    def set_episode_params(self, max_episode_steps: int, reward_scale: float):
+        """Episode length and reward scale of the following steps (Environment.reset's arguments,
+        environment.py:1233, :1258-1259); call before the reset they belong to."""
+        check(self._L.pk_set_episode_params(self._h, int(max_episode_steps), float(reward_scale)), "pk_set_episode_params")
+        self.max_episode_steps, self.reward_scale = int(max_episode_steps), float(reward_scale)
 
     def raise_if_failed(self, env: int | None = None):
         """Raise the exception the reference would have raised for a failed env (PK_ERR_*)."""

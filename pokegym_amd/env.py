@@ -19,6 +19,7 @@ from __future__ import annotations
 import io
 import os
 import random
+from pathlib import Path
 
 import numpy as np
 import torch
@@ -29,6 +30,17 @@ from .dist import EpisodeStats, InfoStats, env_rank, shard_range
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_STATE = os.path.join(HERE, "states", "Bulbasaur.state")  # environment.py:119-120
+
+
+def _session_path(env_id: int) -> Path:
+    """environment.py:130-140: experiments/{running experiment name}/sessions/{env_id}."""
+    name = "default_exp_name"
+    try:
+        with open(os.path.join("experiments", "running_experiment.txt")) as f:
+            name = f.read().strip() or name
+    except OSError:
+        pass
+    return Path("experiments") / name / "sessions" / str(env_id)
 
 
 def _read(path_or_bytes):
@@ -55,6 +67,34 @@ class Environment:
         self.headless = headless
         self.initial_states = [io.BytesIO(state)]   # environment.py:119-120 (the template state)
         self.pokemon_center_save_states = []
+        # video / screenshots (environment.py:123, :128, :140, :200-206, :1244-1249, :1340, :1616)
+        self.save_video = save_video
+        self.screenshot_counter = 0
+        self.reset_count = 0
+        self.env_id = Environment._next_id
+        Environment._next_id += 1
+        self.s_path = Path(kwargs["s_path"]) if "s_path" in kwargs else _session_path(self.env_id)
+        self._recorder = None
+        if save_video:
+            from .video import FrameRecorder
+            self._recorder = FrameRecorder(self.emu, [0])
+
+    _next_id = 0
+
+    def video(self):
+        """environment.py:408-410: the current (144, 160, 3) screen."""
+        from .video import to_rgb
+        return to_rgb(self.emu.screen[0].cpu().numpy())
+
+    def add_video_frame(self):
+        """environment.py:621-622 (the frame stays on the device until the episode is written)."""
+        self._recorder.capture()
+
+    def save_screenshot(self, event, map_n):
+        """environment.py:200-206: screenshots/{counter}_{event}_{map_n}.jpeg."""
+        from .video import save_screenshot
+        self.screenshot_counter += 1
+        return save_screenshot(self.emu.screen[0].cpu().numpy(), event, map_n, self.screenshot_counter)
 
     # -- savestates (environment.py:208-227): PyBoy v9 images of the device state --------------
     def save_state(self):
@@ -80,11 +120,20 @@ class Environment:
         self.emu.load_env(0, data)
 
     def reset(self, seed=None, options=None, max_episode_steps=None, reward_scale=None):
-        """environment.py:1233-1334 (seeding is not supported, as in the reference)."""
-        if max_episode_steps not in (None, self.max_episode_steps) or reward_scale not in (None, self.reward_scale):
-            raise ValueError("max_episode_steps / reward_scale are fixed at construction on the device")
+        """environment.py:1233-1334 (seeding is not supported, as in the reference).  As there,
+        max_episode_steps / reward_scale apply from this reset on (:1258-1259); None keeps the
+        current values (the constructor's, 20480 / 4.0 by default — the reference's reset defaults)."""
+        mes = self.max_episode_steps if max_episode_steps is None else int(max_episode_steps)
+        rsc = self.reward_scale if reward_scale is None else float(reward_scale)
+        if (mes, rsc) != (self.max_episode_steps, self.reward_scale):
+            self.emu.set_episode_params(mes, rsc)
+            self.max_episode_steps, self.reward_scale = mes, rsc
         obs = self.emu.reset()
         self.emu.raise_if_failed(0)
+        if self.save_video:   # a new episode file: {s_path}/reset_{k} (environment.py:1244-1249)
+            self._recorder.clear()
+            self._video_file = self.s_path / f"reset_{self.reset_count}"
+        self.reset_count += 1
         return obs[0].cpu().numpy(), {}
 
     def step(self, action, fast_video=True):
@@ -92,8 +141,13 @@ class Environment:
         holds the numeric scalars of the reference's "stats" and "reward" dicts (pokegym_amd/info.py)."""
         a = torch.tensor([int(action)], dtype=torch.uint8, device=self.emu.device)
         obs, rew, term, trunc = self.emu.step(a)
+        if self.save_video:
+            self.add_video_frame()
         self.emu.raise_if_failed(0)
         done = bool(term[0].item())
+        if self.save_video and done:    # environment.py:1616-1617: the episode's video is closed
+            self.last_video = self._recorder.write(self._video_file)
+            self._recorder.clear()
         info = self.emu.info_dicts([0]).get(0, {})
         if info:   # "pokemon_exploration_map": self.counts_map (float64 in the reference)
             info["pokemon_exploration_map"] = self.emu.heatmap[0].cpu().numpy().astype(np.float64)
@@ -170,7 +224,13 @@ class VecEnv:
     def _range(self, b: int) -> slice:
         return slice(b * self.batch_size, (b + 1) * self.batch_size)
 
-    def reset(self, seed=None):
+    def reset(self, seed=None, max_episode_steps=None, reward_scale=None):
+        """Reset every env; max_episode_steps / reward_scale (Environment.reset's arguments,
+        environment.py:1233) apply to all envs from here on, None keeps the current values."""
+        if max_episode_steps is not None or reward_scale is not None:
+            mes = max_episode_steps if max_episode_steps is not None else getattr(self.emu, "max_episode_steps", 20480)
+            rsc = reward_scale if reward_scale is not None else getattr(self.emu, "reward_scale", 4.0)
+            self.emu.set_episode_params(mes, rsc)
         obs = self.emu.reset()
         self.t = 0
         if self.sticky_errors is not None:
@@ -246,6 +306,12 @@ class VecEnv:
     def load_state(self, env: int, state: bytes):
         """Install a v9 savestate into one env (pk_load_env; pyboy_binding.py:59-69)."""
         self.emu.load_env(env, state)
+
+    def video_recorder(self, envs, capacity: int = 1024):
+        """A FrameRecorder (pokegym_amd/video.py) of the given envs' screens: call .capture() after
+        each step, .write(path, k) at an episode's end (the reference's save_video per env)."""
+        from .video import FrameRecorder
+        return FrameRecorder(self.emu, envs, capacity)
 
     def exploration_map(self, group=None) -> torch.Tensor:
         """Sum of every env's counts_map over all ranks (int64 (444, 436), RCCL all-reduce) — the

@@ -82,3 +82,28 @@ def test_load_state_mid_episode_keeps_step_counter():
                 break
         env.close()
     assert done_at == [5, 5]
+
+
+@pytest.mark.gpu
+def test_environment_reset_takes_episode_params():
+    """Environment.reset(max_episode_steps, reward_scale) (environment.py:1233, :1258-1259) equals an
+    env built with those values: same rewards, done at the same step; a longer episode grows the
+    device's seen-coordinate set."""
+    import numpy as np
+    from pokegym_amd.env import Environment
+    from pokegym_amd.testrom.game import game_rom
+    rom = game_rom()
+    a = Environment(rom_path=rom)
+    b = Environment(rom_path=rom, max_episode_steps=5, reward_scale=2.0)
+    oa, _ = a.reset(max_episode_steps=5, reward_scale=2.0)
+    ob, _ = b.reset()
+    assert np.array_equal(oa, ob)
+    for t, act in enumerate([0, 3, 4, 1, 2]):
+        ra = a.step(act)
+        rb = b.step(act)
+        assert np.array_equal(ra[0], rb[0]) and ra[1] == rb[1] and ra[2] == rb[2] == (t == 4)
+    a.reset(max_episode_steps=50000)          # > the 20,480-step capacity chosen at construction
+    for act in range(3):
+        assert not a.step(act)[2]
+    a.close()
+    b.close()
