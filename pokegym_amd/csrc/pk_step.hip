@@ -710,13 +710,21 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             const u32 r0 = romw[la >> 2], r1 = romw[(la >> 2) + 1u];
             const u32 h0 = lds_hcode[q], h1 = lds_hcode[q + PK_WG_ENVS], h2 = lds_hcode[q + 2u * PK_WG_ENVS];
             pbytes = sel(fh, h0 | (h1 << 8) | (h2 << 16), __builtin_amdgcn_alignbyte(r1, r0, la & 3u));
+            // code in a switchable bank not staged in LDS (most of a 64-bank cartridge's banks): two
+            // dwords of the global ROM (L2-resident), so the microcode entry is still prefetched here
+            // and its LDS latency overlaps the timer/LCD stage like that of staged code
+            const bool fg = !fl & !fh & (npc - 0x4000u < 0x3FFEu);
+            if (fg) {
+                const u32 ga = rom_global_index(A, s, npc);
+                pbytes = __builtin_amdgcn_alignbyte(A.romw[(ga >> 2) + 1u], A.romw[ga >> 2], ga & 3u);
+            }
             const u32 op = pbytes & 0xFFu;
             PK_STAMP_AT(4);
             const u32 di = sel(op == 0xCBu, 256u + ((pbytes >> 8) & 0xFFu), op);
             p0 = ucv[di * 3u];
             p1 = ucv[di * 3u + 1u];
             p2 = ucv[di * 3u + 2u];
-            pf = sel(fl | fh, 1u, 0u);
+            pf = sel(fl | fh | fg, 1u, 0u);
         }
 
         // ---------------- HALT fast-forward, timer, LCD (pyboy mb.tick) ----------------
