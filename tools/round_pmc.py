@@ -1,0 +1,82 @@
+"""Assemble profiles/pmc_<workload>.json (what bench.py reports as roofline.traffic and pmc_stamp)
+from a tools/gpu_round_prof.sh run: K1 HBM bytes per launch (FETCH_SIZE + WRITE_SIZE, units
+calibrated on a 1 GiB copy), VALUBusy / VALUUtilization by rocprofv3's derived-counter formulas
+(gfx94x fallbacks, MI355X_MICROARCH.md §rocprofv3), the wave-parked (s_waitcnt) share, and the
+per-launch K1 time of the stats pass.
+usage: python tools/round_pmc.py gpurun_out/rprof_TAG NAME WORKLOAD_KEY > profiles/pmc_<key>.json"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+CU_NUM, MAX_WAVE = 256, 64
+
+
+def per_dispatch(d, kernel):
+    vals = defaultdict(lambda: defaultdict(float))
+    for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
+        for row in csv.DictReader(open(f)):
+            if row["Kernel_Name"].startswith(kernel):
+                vals[int(row["Dispatch_Id"])][row["Counter_Name"]] += float(row["Counter_Value"])
+    return vals
+
+
+def mean(vals, key, skip_first=True):
+    ids = sorted(vals)
+    if skip_first and len(ids) > 1:
+        ids = ids[1:]   # the first launch starts from the post-reset state
+    xs = [vals[i][key] for i in ids if key in vals[i]]
+    return sum(xs) / len(xs) if xs else None
+
+
+def main():
+    root, name, key = sys.argv[1], sys.argv[2], sys.argv[3]
+    D = os.path.join(root, name)
+    cf = mean(per_dispatch(os.path.join(root, "cfetch"), "__amd_rocclr_copyBuffer"), "FETCH_SIZE", False)
+    cw = mean(per_dispatch(os.path.join(root, "cwrite"), "__amd_rocclr_copyBuffer"), "WRITE_SIZE", False)
+    gib = float(1 << 30)
+    fs, ws = gib / cf, gib / cw          # bytes per FETCH_SIZE / WRITE_SIZE unit (3 copies averaged)
+    f = per_dispatch(os.path.join(D, "fetch"), "pk_step_kernel")
+    w = per_dispatch(os.path.join(D, "write"), "pk_step_kernel")
+    v = per_dispatch(os.path.join(D, "valu"), "pk_step_kernel")
+    rd, wr = mean(f, "FETCH_SIZE") * fs, mean(w, "WRITE_SIZE") * ws
+    # rocprofv3's VALUBusy: 100 * sum(SQ_ACTIVE_INST_VALU) / CU_NUM / max(GRBM_GUI_ACTIVE); the
+    # per-dispatch GRBM_GUI_ACTIVE here is summed over the 8 XCDs, so max = sum / 8
+    busy = 100.0 * mean(v, "SQ_ACTIVE_INST_VALU") / CU_NUM / (mean(v, "GRBM_GUI_ACTIVE") / 8)
+    util = 100.0 * mean(v, "SQ_THREAD_CYCLES_VALU") / (mean(v, "SQ_ACTIVE_INST_VALU") * MAX_WAVE)
+    wait = 100.0 * mean(v, "SQ_WAIT_ANY") / mean(v, "SQ_WAVE_CYCLES")
+    k1 = []
+    for fcsv in glob.glob(os.path.join(D, "stats", "*kernel_stats.csv")):
+        for row in csv.DictReader(open(fcsv)):
+            if row["Name"].startswith("pk_step_kernel"):
+                k1.append(float(row["AverageNs"]) / 1e6)
+    bench = json.loads(open(os.path.join(D, "stats_bench.json")).read().strip().splitlines()[-1])
+    out = {
+        "workload": bench["config"]["workload"],
+        "source": f"{os.path.relpath(root)}/{name} (tools/gpu_round_prof.sh; summarised by tools/round_pmc.py)",
+        "method": "rocprofv3 --kernel-trace --pmc, one pass per counter group; per-dispatch means over the K1 launches "
+                  "after the first; FETCH_SIZE / WRITE_SIZE units calibrated on a 1 GiB device copy (FETCH_SIZE "
+                  "counts half of a wide read on gfx950; the calibration carries that factor)",
+        "calibration": {"FETCH_SIZE_per_GiB": cf, "WRITE_SIZE_per_GiB": cw},
+        "k1_read_bytes": int(rd), "k1_write_bytes": int(wr),
+        "hbm_bytes_per_launch_k1": int(rd + wr),
+        "valu_busy_pct": round(busy, 2),
+        "valu_busy_formula": "100*sum(SQ_ACTIVE_INST_VALU)/CU_NUM/max(GRBM_GUI_ACTIVE) (rocprofv3 VALUBusy, gfx94x form)",
+        "valu_utilization_pct": round(util, 2),
+        "valu_utilization_formula": "100*sum(SQ_THREAD_CYCLES_VALU)/(sum(SQ_ACTIVE_INST_VALU)*64): active lanes per VALU "
+                                    "instruction (K1 runs 32 envs in each 64-lane wave at 65,536 envs, so <= 50 %)",
+        "wait_any_pct": round(wait, 2),
+        "waves_per_launch": mean(v, "SQ_WAVES"),
+        "k1_avg_ms_rocprof_stats": round(k1[0], 3) if k1 else None,
+        "bench_under_rocprof": {"value": bench["value"], "k1_ms": bench["roofline"]["k1_ms"],
+                                "span_ms": bench["roofline"]["span_ms"]},
+        "note": "K1 loads/stores single bytes from divergent lanes (lane-interleaved images), an access width the "
+                "1 GiB-copy calibration does not cover: the byte totals are request-granular upper estimates",
+    }
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
