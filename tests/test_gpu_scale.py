@@ -129,3 +129,31 @@ def test_config5_shard_32768_envs_reward_reload():
     assert (got_obs[live_obs] == obs_d[live_obs]).all()
     # resets fired where the reference's done did: time >= 3 after steps 3 and 6
     assert (done[2][live[2]] == 1).all() and (done[5][live[5]] == 1).all()
+
+
+def test_config4_shard_vecenv_sub_batches():
+    """configs[3] per-GPU shard through the PufferLib surface: 32,768 envs, screen obs, stepped as
+    2 sub-batches of 16,384 on their own streams (the bench's config4) == the same envs stepped as
+    one batch (screens, dones, whole-machine digests of every env)."""
+    import torch
+    from pokegym_amd.env import VecEnv
+    from pokegym_amd.testrom.game import game_rom
+    rom, n, steps = game_rom(), 32768, 3
+    acts = torch.from_numpy(np.random.default_rng(3276).integers(0, 8, (steps, n), dtype=np.uint8)).cuda()
+    kw = dict(rom=rom, power_on=True, reward=False, max_episode_steps=2, log_interval=0)
+    full = VecEnv(n, **kw)
+    sub = VecEnv(n, batch_size=n // 2, **kw)
+    full.async_reset()
+    sub.async_reset()
+    for t in range(steps):
+        full.recv()
+        full.send(acts[t])
+        for _ in range(2):
+            sub.recv()
+            sub.send(acts[t, sub.current_envs()])
+    torch.cuda.synchronize()
+    assert torch.equal(full.emu.screen, sub.emu.screen)
+    assert torch.equal(full.emu.terminals, sub.emu.terminals) and bool(full.emu.terminals.any())
+    assert np.array_equal(gpu_digests(full.emu), gpu_digests(sub.emu))
+    full.close()
+    sub.close()
