@@ -138,7 +138,7 @@ def test_config4_shard_vecenv_sub_batches():
     import torch
     from pokegym_amd.env import VecEnv
     from pokegym_amd.testrom.game import game_rom
-    rom, n, steps = game_rom(), 32768, 3
+    rom, n, steps = game_rom(), 32768, 4
     acts = torch.from_numpy(np.random.default_rng(3276).integers(0, 8, (steps, n), dtype=np.uint8)).cuda()
     kw = dict(rom=rom, power_on=True, reward=False, max_episode_steps=2, log_interval=0)
     full = VecEnv(n, **kw)
