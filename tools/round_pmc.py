@@ -55,6 +55,8 @@ def main():
     bench = json.loads(open(os.path.join(D, "stats_bench.json")).read().strip().splitlines()[-1])
     out = {
         "workload": bench["config"]["workload"],
+        "envs_per_gpu": bench["config"]["envs_per_gpu"],
+        "rom": bench["config"]["rom"],
         "source": f"{os.path.relpath(root)}/{name} (tools/gpu_round_prof.sh; summarised by tools/round_pmc.py)",
         "method": "rocprofv3 --kernel-trace --pmc, one pass per counter group; per-dispatch means over the K1 launches "
                   "after the first; FETCH_SIZE / WRITE_SIZE units calibrated on a 1 GiB device copy (FETCH_SIZE "
