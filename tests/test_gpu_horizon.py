@@ -76,3 +76,31 @@ def test_horizon_10k_segments(horizon, part):
             bad.append((int(step), int(j)))
     assert not bad, f"{len(bad)} (step, trajectory) checkpoints differ: {bad[:8]}"
     st["ok"] = True
+
+
+def test_horizon_64_bank_rom():
+    """The 1 MiB pkbench layout (overworld engine in 60 unstaged switchable banks: global-ROM fetch
+    and reads, Bankswitch every frame) over 2,000 scripted steps: 64 trajectories in 8 segments of
+    250 steps run side by side, whole v9 state compared with the oracle at every segment end."""
+    import torch
+    from pokegym_amd.emulator import BatchedEmulator
+    from pokegym_amd.testrom.game import game_rom
+    rom = game_rom(64)
+    total, segs, ntraj = 2000, 8, 64
+    seg = total // segs
+    actions = horizon_actions(total, ntraj)
+    with OP.pool() as ex:
+        dig, keep = OP.trajectories(ex, rom, None, actions, every=seg, keep_every=seg, chunk=4)
+    emu = BatchedEmulator(rom, segs * ntraj, render=True)
+    for k in range(1, segs):
+        for j in range(ntraj):
+            emu.load_env(k * ntraj + j, keep[(k, j)])
+    table = np.concatenate([actions[k * seg:(k + 1) * seg] for k in range(segs)], axis=1)
+    acts = torch.from_numpy(np.ascontiguousarray(table)).to(emu.device)
+    for t in range(seg):
+        emu.step(acts[t])
+    torch.cuda.synchronize()
+    got = oracle.state_digests(emu.snapshot_range(0, emu.n)).reshape(segs, ntraj)
+    emu.close()
+    bad = [(k, int(j)) for k in range(segs) for j in np.nonzero(got[k] != dig[k])[0]]
+    assert not bad, f"{len(bad)} (segment, trajectory) states differ: {bad[:8]}"
