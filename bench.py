@@ -255,6 +255,7 @@ def main():
             stamp, stamp_src = None, None   # the committed passes profiled another env count
         out = {
             "metric": "aggregate env.step/sec",
+            "per_gpu_value": round(value / world, 1),
             "value": round(value, 1),
             "unit": "env-steps/s",
             "n_gpus": world,
@@ -277,6 +278,9 @@ def main():
                 "release_frame": 8,
                 "max_episode_steps": max_steps,
                 "parallelism": f"envs sharded over {world} GPU(s), no data-path collective",
+                "scaling_note": ("the default workload is config3 (65,536 envs/GPU) at N=1 and config4 (the configs[3] "
+                                 "shard, 32,768 envs/GPU) at N>1; compare N>1 per-GPU rates with the N=1 config4 line "
+                                 "(python bench.py --workload config4), not with config3"),
             },
             "roofline": {
                 "bound": "hbm",
