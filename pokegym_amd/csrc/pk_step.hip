@@ -659,6 +659,17 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             // IME / HALT / CRASH / QUEUED: (cpu & keep) | set from the microcode
             s.cpu = (s.cpu & (0xFFFFFFF0u | ((K >> PK_KB_CPUAND) & 15u))) | (K >> PK_KB_CPUOR);
         }
+        // next instruction in an unstaged switchable bank (most of a 64-bank cartridge): its two
+        // global-ROM dwords are requested now, so their latency overlaps the write stage (a lane
+        // whose write switches the ROM bank refetches at the top of the next iteration)
+        u32 ng0 = 0, ng1 = 0, nga = 0;
+        const bool nfg = !(s.pc < 0x4000u || (s.pc < 0x8000u && s.rb != PK_NO_BANK)) & (s.pc - 0x4000u < 0x3FFEu)
+                       & !(s.pc - 0xFF80u < 0x7Du);
+        if (nfg) {
+            nga = rom_global_index(A, s, s.pc);
+            ng0 = A.romw[nga >> 2];
+            ng1 = A.romw[(nga >> 2) + 1u];
+        }
 
         // ---------------- memory writes (wv0 at addr0, wv1 at addr1) ----------------
         const bool wr = bit(D, PK_DB_WR) != 0u && taken != 0u, wr2 = bit(D, PK_DB_WR2) != 0u;
@@ -713,11 +724,8 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             // code in a switchable bank not staged in LDS (most of a 64-bank cartridge's banks): two
             // dwords of the global ROM (L2-resident), so the microcode entry is still prefetched here
             // and its LDS latency overlaps the timer/LCD stage like that of staged code
-            const bool fg = !fl & !fh & (npc - 0x4000u < 0x3FFEu);
-            if (fg) {
-                const u32 ga = rom_global_index(A, s, npc);
-                pbytes = __builtin_amdgcn_alignbyte(A.romw[(ga >> 2) + 1u], A.romw[ga >> 2], ga & 3u);
-            }
+            const bool fg = nfg & !(wr & !wram);   // unchanged bank (no slow write) and still unstaged
+            pbytes = sel(fg, __builtin_amdgcn_alignbyte(ng1, ng0, nga & 3u), pbytes);
             const u32 op = pbytes & 0xFFu;
             PK_STAMP_AT(4);
             const u32 di = sel(op == 0xCBu, 256u + ((pbytes >> 8) & 0xFFu), op);
