@@ -752,12 +752,32 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             lcd_unfold(s);
             const u32 cpu = s.cpu, stat = bfe8(s.lcd0, 8), ly = bfe8(s.lcd0, 16), nm = (s.lcd2 >> 24) & 3u;
             const bool cand = !(cpu & CPU_QUEUED) && ((cpu >> 8) & (cpu >> 16) & 0x1Fu) == 0u
-                           && (s.lcd0 & 0x80u) && (stat & 0x68u) == 0u && !(tac & 4u) && !s.render && ly < 143u && nm != 1u && s.clock <= s.target;
+                           && (s.lcd0 & 0x80u) && (stat & 0x68u) == 0u && !(tac & 4u) && ly < 143u && nm != 1u && s.clock <= s.target;
             const u32 lines = 143u - ly;
             const u32 vbl = sel(nm == 2u, s.target + 456u * lines, s.target - sel(nm == 3u, 80u, 250u) + 456u * (lines + 1u));
             const u32 nev = sel(nm == 3u, 2u, sel(nm == 0u, 1u, 0u)) + 3u * lines + 1u;  // iterations up to VBlank
             const u32 tnew = vbl - 206u;                                                  // line 143 mode-0 event
             if (cand && budget + (vbl - s.clock) + nev <= 16u * FRAME_CYCLES) {
+                if (s.render) {
+                    // rendered frame: the skipped mode-0 events would latch every remaining line with
+                    // the (unchanging, the CPU is halted) scroll/window/palette registers — latch
+                    // them here, advancing the window line counter as the per-event latch does
+                    const u32 lcdc = s.lcd0 & 0xFFu, wy = bfe8(s.lcd1, 16), wx = bfe8(s.lcd1, 24);
+                    const u32 l0 = lcdc | (bfe8(s.lcd1, 8) << 8) | (bfe8(s.lcd1, 0) << 16) | (wx << 24);
+                    const u32 l1 = wy | ((s.lcd2 & 0xFFFFFFu) << 8);
+                    const bool wline = (lcdc & 0x20u) && (int)wx - 7 < (int)PK_COLS;
+                    int lw = (int)bfe8(s.misc, 16) - 1;
+                    const u32 y0 = sel(nm == 2u, ly + 1u, ly);   // nm 2: this line's mode-0 event has passed
+                    for (u32 y = y0; y < PK_ROWS; y++) {
+                        if (wline && wy <= y) lw += 1;
+                        const u32 idx = (c.gid * PK_ROWS + y) * PK_LANES + c.lane;
+                        A.lat[idx] = l0;
+                        A.lat[A.lat_stride + idx] = l1;
+                        A.lat[2u * A.lat_stride + idx] = (u32)(lw + 1) | 0x100u;
+                    }
+                    s.misc = setb8(s.misc, 16, 0u);              // reset after line 143
+                    s.npend += PK_ROWS - y0;
+                }
                 const u32 skipped = tnew - s.clock;
                 s.divacc = (s.divacc + skipped) & 0xFFFFu;
                 budget += skipped + (nev - 1u);
