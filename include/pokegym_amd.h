@@ -103,10 +103,13 @@ int pk_step(pk_handle* h, const uint8_t* actions_dev, uint8_t* screen_dev, doubl
             uint8_t* term_dev, uint8_t* trunc_dev, void* stream);
 
 /* Sub-batch forms (PufferLib batch_size < num_envs, README.md:116-118: 72 envs stepped 24 at a
- * time): the same step / reset restricted to envs [env0, env0 + count).  env0 and env0 + count
- * are multiples of 64 (or the end is n).  All arrays stay full-size (device u8/f64[n]); only the
- * range's elements are read or written, so disjoint ranges may run concurrently on different
- * streams (each range has its own reset lists). */
+ * time): the same step / reset restricted to envs [env0, env0 + count).  env0 is a multiple of
+ * 64 (a 64-env image group); the end may be anywhere up to n.  All arrays stay full-size (device
+ * u8/f64[n]); only the range's elements are read or written, so disjoint ranges may run
+ * concurrently on different streams (each range has its own reset lists).  A range that ends
+ * inside a group leaves the rest of that group untouched; a caller that steps those envs
+ * concurrently in another range cannot (no range starts inside a group), so sub-batches of any
+ * size are laid out one per group-aligned slot (pokegym_amd VecEnv pads 24-env sub-batches to 64). */
 int pk_step_range(pk_handle* h, uint32_t env0, uint32_t count, const uint8_t* actions_dev, double* rew_dev,
                   uint8_t* term_dev, uint8_t* trunc_dev, void* stream);
 int pk_reset_range(pk_handle* h, uint32_t env0, uint32_t count, const uint8_t* env_mask_dev, void* stream);

@@ -496,8 +496,8 @@ static int template_reset(pk_handle* h, const uint8_t* mask, uint32_t env0, uint
 
 static int check_range(pk_handle* h, uint32_t env0, uint32_t count) {
     if (!h) return fail(-EINVAL, "null handle");
-    if (count == 0 || env0 % PK_LANES || (uint64_t)env0 + count > h->n || ((env0 + count) % PK_LANES && env0 + count != h->n))
-        return fail(-EINVAL, "env range [%u, +%u): start and end must be multiples of 64 (or the end n = %u)", env0, count, h->n);
+    if (count == 0 || env0 % PK_LANES || (uint64_t)env0 + count > h->n)
+        return fail(-EINVAL, "env range [%u, +%u): the start must be a multiple of 64 and the end <= n = %u", env0, count, h->n);
     return 0;
 }
 

@@ -886,6 +886,9 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
     }
 #endif
     if (!active) return;
+    // lanes past the range's end (in its last 64-env group) ran nothing and write nothing back:
+    // those envs may belong to nobody else, but the range does not own them
+    if (!active) return;
     lcd_unfold(s);
     R[PK_R_W0 * np + env] = s.w0;
     R[PK_R_W1 * np + env] = perm(s.w1, s.w1, 0x02030100u);

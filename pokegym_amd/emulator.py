@@ -116,7 +116,7 @@ class BatchedEmulator:
 
     def step_range(self, env0: int, actions: torch.Tensor):
         """One env-step of the sub-batch [env0, env0 + len(actions)) only (pk_step_range), on the
-        current stream: env0 and the end are multiples of 64 (or the end is n).  Returns views of
+        current stream: env0 is a multiple of 64, the end anywhere up to n.  Returns views of
         the sub-batch's (obs, rewards, terminals, truncations)."""
         count = actions.numel()
         sl = slice(env0, env0 + count)

@@ -168,10 +168,12 @@ class VecEnv:
     trains 72 envs 24 at a time, README.md:116-118): recv() returns the next sub-batch whose step
     has finished, send(actions) steps the sub-batch the last recv() returned on its own HIP stream
     (pk_step_range) and returns immediately, so the policy works on one sub-batch while the GPU
-    steps the others.  batch_size must divide num_envs and be a multiple of 64.  step(actions)
-    steps all envs at once (batch_size == num_envs).  Sub-batches overlap on the GPU while the HIP
-    runtime has a hardware queue per stream (GPU_MAX_HW_QUEUES, 4 by default: the default stream plus
-    up to 3 sub-batches; beyond that streams share queues and their launches serialise)."""
+    steps the others.  batch_size must divide num_envs; a sub-batch starts on a 64-env image group
+    (pk_step_range), so a batch_size that is not a multiple of 64 (the reference's 24) is laid out
+    in 64-aligned slots whose padding envs are never stepped.  step(actions) steps all envs at once.
+    Sub-batches overlap on the GPU while the HIP runtime has a hardware queue per stream
+    (GPU_MAX_HW_QUEUES, 4 by default: the default stream plus up to 3 sub-batches; beyond that
+    streams share queues and their launches serialise)."""
 
     def __init__(self, num_envs: int, rom_path=None, state_path=None, rom: bytes | None = None, state: bytes | None = None,
                  device: int | None = None, max_episode_steps: int = 20480, reward_scale: float = 4.0,
@@ -180,6 +182,14 @@ class VecEnv:
         """reward=False: the screen-obs env of configs[3] — obs is the (144, 160) u8 screen, rewards are
         0 and episodes end at max_episode_steps.  power_on=True starts (and resets) every env from
         the cartridge's power-on state instead of a savestate."""
+        self.batch_size = batch_size or num_envs
+        if num_envs % self.batch_size:
+            raise ValueError("batch_size must divide num_envs")
+        self.num_batches = num_envs // self.batch_size
+        # slot of a sub-batch in the emulator: batch_size rounded up to a 64-env group
+        self.slot = (self.batch_size if self.num_batches == 1 or self.batch_size % 64 == 0
+                     else -(-self.batch_size // 64) * 64)
+        n_phys = self.num_batches * self.slot
         if emulator is None:
             from .emulator import BatchedEmulator
             rom = rom if rom is not None else _read(rom_path or "pokemon_red.gb")
@@ -187,16 +197,18 @@ class VecEnv:
                 state = None
             else:
                 state = state if state is not None else _read(state_path if state_path is not None else DEFAULT_STATE)
-            emulator = BatchedEmulator(rom, num_envs, state=state, device=0 if device is None else device, render=True,
+            emulator = BatchedEmulator(rom, n_phys, state=state, device=0 if device is None else device, render=True,
                                        reward=reward, max_episode_steps=max_episode_steps, reward_scale=reward_scale,
                                        reload_on_reset=reload_on_reset, heatmap=heatmap)
+        if getattr(emulator, "n", n_phys) != n_phys:
+            raise ValueError(f"the emulator must hold {n_phys} envs ({self.num_batches} sub-batch slots of {self.slot})")
         self.emu = emulator
         self.device = emulator.device
         self.num_envs = self.num_agents = num_envs
-        self.batch_size = batch_size or num_envs
-        if num_envs % self.batch_size or (self.batch_size != num_envs and self.batch_size % 64):
-            raise ValueError("batch_size must divide num_envs and be a multiple of 64")
-        self.num_batches = num_envs // self.batch_size
+        # emulator index of every env (only differs from the env index when slots are padded)
+        self._padded = n_phys != num_envs
+        self._phys = (torch.cat([torch.arange(b * self.slot, b * self.slot + self.batch_size)
+                                 for b in range(self.num_batches)]).to(self.device) if self._padded else None)
         self.single_observation_space = (spaces.observation_space() if getattr(emulator, "reward", True)
                                          else spaces.screen_space())
         self.single_action_space = spaces.action_space()
@@ -224,6 +236,17 @@ class VecEnv:
     def _range(self, b: int) -> slice:
         return slice(b * self.batch_size, (b + 1) * self.batch_size)
 
+    def _prange(self, b: int) -> slice:
+        """Emulator envs of sub-batch b."""
+        return slice(b * self.slot, b * self.slot + self.batch_size)
+
+    def phys(self, env: int) -> int:
+        """Emulator index of env."""
+        return (env // self.batch_size) * self.slot + env % self.batch_size
+
+    def _logical(self, obs: torch.Tensor) -> torch.Tensor:
+        return obs.index_select(0, self._phys) if self._padded else obs
+
     def reset(self, seed=None, max_episode_steps=None, reward_scale=None):
         """Reset every env; max_episode_steps / reward_scale (Environment.reset's arguments,
         environment.py:1233) apply to all envs from here on, None keeps the current values."""
@@ -231,7 +254,7 @@ class VecEnv:
             mes = max_episode_steps if max_episode_steps is not None else getattr(self.emu, "max_episode_steps", 20480)
             rsc = reward_scale if reward_scale is not None else getattr(self.emu, "reward_scale", 4.0)
             self.emu.set_episode_params(mes, rsc)
-        obs = self.emu.reset()
+        obs = self._logical(self.emu.reset())
         self.t = 0
         if self.sticky_errors is not None:
             self.sticky_errors.zero_()
@@ -244,25 +267,26 @@ class VecEnv:
         bad = torch.nonzero(self.sticky_errors).flatten()
         if bad.numel():
             from ._native import ERR_EXCEPTIONS
-            e = int(bad[0])
-            code = int(self.sticky_errors[e])
+            p = int(bad[0])
+            code = int(self.sticky_errors[p])
+            e = (p // self.slot) * self.batch_size + p % self.slot
             self.sticky_errors.zero_()
             raise ERR_EXCEPTIONS.get(code, RuntimeError)(
                 f"env {e}: reference reward stack raises here (PK_ERR {code}); {bad.numel()} env(s) failed")
 
     def _step_range(self, b: int, actions: torch.Tensor):
         """Step sub-batch b (envs _range(b)) on the current stream, then book-keep and auto-reset."""
-        sl = self._range(b)
+        sl, psl = self._range(b), self._prange(b)
         if self.num_batches == 1:
             obs, rew, term, trunc = self.emu.step(actions)
         else:
-            obs, rew, term, trunc = self.emu.step_range(sl.start, actions)
+            obs, rew, term, trunc = self.emu.step_range(psl.start, actions)
         self.stats.update(rew, term, batch=b, envs=sl)
         if self.info_stats is not None:
-            self.info_stats.update(self.emu.info[:, sl], self.emu.info_flag[sl], batch=b)
+            self.info_stats.update(self.emu.info[:, psl], self.emu.info_flag[psl], batch=b)
         if self.sticky_errors is not None:
-            se = self.sticky_errors[sl]
-            torch.where(se != 0, se, self.emu.errors[sl], out=se)
+            se = self.sticky_errors[psl]
+            torch.where(se != 0, se, self.emu.errors[psl], out=se)
         rewards = rew.clone()
         terminals = term.to(torch.bool)
         truncations = trunc.to(torch.bool)
@@ -270,7 +294,7 @@ class VecEnv:
         if self.num_batches == 1:
             self.emu.reset(term)
         else:
-            self.emu.reset_range(sl.start, self.batch_size, self.emu.terminals)
+            self.emu.reset_range(psl.start, self.batch_size, self.emu.terminals)
         return obs, rewards, terminals, truncations
 
     def _log(self):
@@ -291,7 +315,7 @@ class VecEnv:
             obs, rewards, terminals, truncations = self._step_range(0, a)
         else:
             outs = [self._step_range(b, a[self._range(b)]) for b in range(self.num_batches)]
-            obs = self.emu.obs if self.emu.reward else self.emu.screen
+            obs = self._logical(self.emu.obs if self.emu.reward else self.emu.screen)
             rewards = torch.cat([o[1] for o in outs])
             terminals = torch.cat([o[2] for o in outs])
             truncations = torch.cat([o[3] for o in outs])
@@ -301,17 +325,17 @@ class VecEnv:
 
     def save_state(self, env: int) -> bytes:
         """PyBoy v9 savestate of one env (pk_snapshot; environment.py:208-213 per env)."""
-        return self.emu.snapshot(env)
+        return self.emu.snapshot(self.phys(env))
 
     def load_state(self, env: int, state: bytes):
         """Install a v9 savestate into one env (pk_load_env; pyboy_binding.py:59-69)."""
-        self.emu.load_env(env, state)
+        self.emu.load_env(self.phys(env), state)
 
     def video_recorder(self, envs, capacity: int = 1024):
         """A FrameRecorder (pokegym_amd/video.py) of the given envs' screens: call .capture() after
         each step, .write(path, k) at an episode's end (the reference's save_video per env)."""
         from .video import FrameRecorder
-        return FrameRecorder(self.emu, envs, capacity)
+        return FrameRecorder(self.emu, [self.phys(int(e)) for e in envs], capacity)
 
     def exploration_map(self, group=None) -> torch.Tensor:
         """Sum of every env's counts_map over all ranks (int64 (444, 436), RCCL all-reduce) — the
@@ -358,7 +382,7 @@ class VecEnv:
         rew, term, trunc = self._pending[b]
         obs = self.emu.obs if self.emu.reward else self.emu.screen
         infos, self._pending_infos = getattr(self, "_pending_infos", []), []
-        return obs[sl], rew, term, trunc, infos, self.env_ids[sl], self.masks[sl]
+        return obs[self._prange(b)], rew, term, trunc, infos, self.env_ids[sl], self.masks[sl]
 
     def current_envs(self) -> slice:
         """Local env range of the sub-batch the last recv() returned (host-side, no sync)."""

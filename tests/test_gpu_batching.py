@@ -43,15 +43,17 @@ def test_step_range_on_streams_matches_full_batch():
     sub.close()
 
 
-def test_vecenv_sub_batches_match_full_batch():
-    """VecEnv(256, batch_size=64) driven through async_reset/recv/send with the reward stack,
+@pytest.mark.parametrize("n,bs", [(256, 64), (72, 24)])
+def test_vecenv_sub_batches_match_full_batch(n, bs):
+    """VecEnv(n, batch_size=bs) driven through async_reset/recv/send with the reward stack,
     template reload on done (max_episode_steps 3) and auto-reset: every sub-batch's rewards,
-    dones and observations equal those of the same envs in a full-batch VecEnv."""
+    dones and observations equal those of the same envs in a full-batch VecEnv.  (72, 24) is the
+    reference's own setting (README.md:116-118): sub-batches in padded 64-env slots."""
     import torch
     from pokegym_amd.env import VecEnv
     from pokegym_amd.testrom.game import game_rom
     rom, state = game_rom(), open(STATE, "rb").read()
-    n, bs, rounds = 256, 64, 7
+    rounds = 7
     acts = torch.from_numpy(np.random.default_rng(12).integers(0, 8, (rounds, n), dtype=np.uint8)).cuda()
     kw = dict(rom=rom, state=state, max_episode_steps=3, reload_on_reset=True, log_interval=0)
     full = VecEnv(n, **kw)
@@ -79,5 +81,35 @@ def test_vecenv_sub_batches_match_full_batch():
             assert torch.equal(o, f_obs[sl]), (rnd, e0)
             sub.send(acts[min(rnd + 1, rounds - 1), ids])
     assert dones == 2 * n   # every episode ended (and was reloaded) twice inside the run
+    full.close()
+    sub.close()
+
+
+def test_vecenv_padded_slots_step_and_savestates():
+    """VecEnv(72, batch_size=24) (sub-batches in padded 64-env slots): step() over all envs returns
+    the envs in env order, equal to an unpadded VecEnv(72); save_state/load_state address envs by
+    their env index."""
+    import torch
+    from pokegym_amd.env import VecEnv
+    from pokegym_amd.testrom.game import game_rom
+    rom, state = game_rom(), open(STATE, "rb").read()
+    kw = dict(rom=rom, state=state, max_episode_steps=4, reload_on_reset=True, log_interval=0)
+    full, sub = VecEnv(72, **kw), VecEnv(72, batch_size=24, **kw)
+    assert sub._padded and sub.emu.n == 3 * 64 and not full._padded
+    fo, _ = full.reset()
+    so, _ = sub.reset()
+    assert torch.equal(fo, so)
+    acts = torch.from_numpy(np.random.default_rng(13).integers(0, 8, (6, 72), dtype=np.uint8)).cuda()
+    for t in range(6):
+        f = full.step(acts[t])
+        s = sub.step(acts[t])
+        for x, y in zip(f[:4], s[:4]):
+            assert torch.equal(x, y), t
+    torch.cuda.synchronize()
+    for e in (0, 23, 24, 47, 71):
+        assert full.save_state(e) == sub.save_state(e), e
+    st = full.save_state(5)
+    sub.load_state(50, st)
+    assert sub.save_state(50) == st
     full.close()
     sub.close()
