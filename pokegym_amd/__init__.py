@@ -6,3 +6,12 @@ Public surface:
   pokegym_amd.env.VecEnv                 PufferLib-shaped batched surface
 """
 __version__ = "0.1.0"
+
+
+def __getattr__(name):
+    """`from pokegym_amd import Environment, Base` as `from pokegym import Base, Environment`
+    (pokegym/__init__.py); loaded on first use so importing the package needs no GPU."""
+    if name in ("Environment", "Base", "VecEnv"):
+        from . import env
+        return env.VecEnv if name == "VecEnv" else env.Environment
+    raise AttributeError(name)

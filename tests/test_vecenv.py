@@ -87,3 +87,85 @@ def test_vecenv_error_survives_autoreset():
     env.step(torch.zeros(3, dtype=torch.uint8))
     with pytest.raises(KeyError):
         env.step(torch.zeros(3, dtype=torch.uint8))   # raised at the logging interval
+
+
+class FakeRangeEmu(FakeEmu):
+    """FakeEmu with the sub-batch entry points (step_range / reset_range on full-size arrays)."""
+    reward = True
+
+    def __init__(self, n, done_every=3):
+        super().__init__(n, done_every)
+        self.rewards = torch.zeros(n, dtype=torch.float64)
+        self.terminals = torch.zeros(n, dtype=torch.uint8)
+        self.truncations = torch.zeros(n, dtype=torch.uint8)
+        self.stepped = torch.zeros(n, dtype=torch.int64)
+
+    def step_range(self, env0, a):
+        sl = slice(env0, env0 + a.numel())
+        self.time[sl] += 1
+        self.stepped[sl] += 1
+        self.obs[sl] = a.view(-1, 1, 1, 1)
+        self.rewards[sl] = a.to(torch.float64)
+        self.terminals[sl] = (self.time[sl] % self.done_every == 0).to(torch.uint8)
+        self.truncations[sl] = self.terminals[sl]
+        return self.obs[sl], self.rewards[sl], self.terminals[sl], self.truncations[sl]
+
+    def reset_range(self, env0, count, mask=None):
+        m = torch.zeros(self.n, dtype=torch.bool)
+        m[env0:env0 + count] = True if mask is None else mask[env0:env0 + count].to(torch.bool)
+        self.time[m] = 0
+        self.obs[m] = 7
+        return self.obs[env0:env0 + count]
+
+
+class _NoStream:
+    """CPU stand-in for the HIP streams/events of the sub-batch pipeline."""
+    def __init__(self, *a, **k):
+        pass
+
+    def wait_stream(self, other):
+        pass
+
+    def wait_event(self, ev):
+        pass
+
+    def record(self, stream=None):
+        pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+def test_vecenv_padded_sub_batch_slots(monkeypatch):
+    """batch_size 24 (the reference's 72 envs in batches of 24, README.md:116-118): each sub-batch
+    sits in its own 64-env slot; step() and recv() address envs by env index, padding never steps."""
+    import pytest
+    for name in ("Stream", "Event", "current_stream", "stream"):
+        monkeypatch.setattr(torch.cuda, name, _NoStream)
+    monkeypatch.setattr(torch.Tensor, "record_stream", lambda self, s: None)
+    with pytest.raises(ValueError):
+        VecEnv(72, emulator=FakeRangeEmu(72), batch_size=24)      # needs 3 slots of 64
+    emu = FakeRangeEmu(3 * 64)
+    env = VecEnv(72, emulator=emu, batch_size=24, log_interval=0)
+    assert env.slot == 64 and [env.phys(e) for e in (0, 23, 24, 47, 48, 71)] == [0, 23, 64, 87, 128, 151]
+    obs, _ = env.reset()
+    assert obs.shape[0] == 72
+    a = torch.arange(72, dtype=torch.uint8)
+    obs, rew, term, trunc, _ = env.step(a)
+    assert torch.equal(rew, a.to(torch.float64)) and torch.equal(obs[:, 0, 0, 0], a)
+    pad = torch.ones(192, dtype=torch.bool)
+    pad[[env.phys(e) for e in range(72)]] = False
+    assert (emu.stepped[pad] == 0).all() and (emu.stepped[~pad] == 1).all()
+    env.async_reset()
+    for _ in range(3):
+        o, r, d, t, infos, ids, m = env.recv()
+        assert o.shape[0] == 24 and ids.numel() == 24
+        env.send(ids.to(torch.uint8))
+    for _ in range(3):
+        o, r, d, t, infos, ids, m = env.recv()
+        assert torch.equal(r, ids.to(torch.float64)) and torch.equal(o[:, 0, 0, 0], ids.to(torch.uint8))
+        env.send(ids.to(torch.uint8))
+    assert (emu.stepped[pad] == 0).all()
