@@ -338,10 +338,10 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
             h->wave_lanes = (uint32_t)v;
         }
         // K1 workgroup size override (parity tests run the benchmarked 512-thread shape at small n):
-        // a multiple of 64 whose envs fit the 256-env HRAM mirror of a workgroup
+        // a multiple of 64 whose envs fit the 512-env HRAM mirror of a workgroup
         if (const char* bl = getenv("PK_K1_BLOCK")) {
             int v = atoi(bl);
-            if (v < 64 || v > 512 || (v % 64) || (uint32_t)(v / 64) * (h->wave_lanes ? h->wave_lanes : 32u) > 256u) {
+            if (v < 64 || v > 512 || (v % 64) || (uint32_t)(v / 64) * (h->wave_lanes ? h->wave_lanes : 32u) > 512u) {
                 delete h;
                 return fail(-EINVAL, "PK_K1_BLOCK must be a multiple of 64 in [64, 512] with (block/64)*wave_lanes <= 256");
             }

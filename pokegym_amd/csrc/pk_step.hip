@@ -34,8 +34,8 @@
 #define CPU_QUEUED 4u
 #define CPU_CRASH 8u
 #define PK_NO_BANK 0xFFFFFFFFu
-// largest K1 workgroup: 256 envs per CU share one LDS copy of the ROM banks and microcode, so a
-// 16-lane wave shape needs 1024-thread workgroups (and <= 128 VGPRs)
+// largest K1 workgroup (one per CU: its envs share one LDS copy of the ROM banks and microcode):
+// 512 threads = 8 waves, two per SIMD at 221 VGPRs
 #ifndef PK_K1_MAX_THREADS
 #define PK_K1_MAX_THREADS 512
 #endif
@@ -75,13 +75,17 @@ enum {
 __shared__ __attribute__((aligned(16))) u32 lds_uc[PK_UC_ENTRIES * PK_UE_WORDS];  // microcode
 __shared__ __attribute__((aligned(16))) u8 lds_rom[PK_LDS_SLOTS * 0x4000u + 16u]; // ROM banks (+ fetch overrun pad)
 __shared__ int8_t lds_slot[128];                                                  // bank -> slot
-// Fetch-only mirror of HRAM (0xFF80-0xFFFE) per env of the workgroup, byte (addr - 0xFF80) * 256 +
-// local env, + one dummy row: the OAM-DMA wait loop runs from HRAM, and fetching it from the HBM
-// image put a second dependent HBM round trip (fetch, then data) into ~30 % of wave iterations.
-// Data reads/writes stay on the image (authoritative); every HRAM write also updates the mirror
-// (lanes that do not write HRAM store to the dummy row, so the store needs no branch).
-#define PK_WG_ENVS 256u
-__shared__ u8 lds_hcode[128u * PK_WG_ENVS];
+// Fetch-only mirror of the first PK_HC_ROWS bytes of HRAM (0xFF80-0xFF9F: where games put the
+// OAM-DMA routine, pokered's hDMARoutine included) per env of the workgroup, byte
+// (addr - 0xFF80) * PK_WG_ENVS + local env, + one dummy row: the OAM-DMA wait loop runs from HRAM,
+// and fetching it from the HBM image put a second dependent HBM round trip (fetch, then data) into
+// ~30 % of wave iterations.  Code elsewhere in HRAM is fetched from the image.  Data reads/writes
+// stay on the image (authoritative); every HRAM write also updates the mirror (lanes that do not
+// write a mirrored byte store to the dummy row, so the store needs no branch).  Up to 512 envs per
+// workgroup: 64-env waves two per SIMD when a launch has the envs for it (>= 131,072).
+#define PK_WG_ENVS 512u
+#define PK_HC_ROWS 32u
+__shared__ u8 lds_hcode[(PK_HC_ROWS + 1u) * PK_WG_ENVS];
 
 // ---------------------------------------------------------------------------------------------
 // branch-free helpers: arguments are evaluated unconditionally, so ?: on them is a v_cndmask
@@ -121,9 +125,9 @@ struct Ctx {
 
 __device__ __forceinline__ u32 ld_img(const Ctx& c, u32 phys) { return c.g[phys * PK_LANES + c.lane]; }
 __device__ __forceinline__ void st_img(const Ctx& c, u32 phys, u32 v) { c.g[phys * PK_LANES + c.lane] = (u8)v; }
-// keep the HRAM fetch mirror in step with a RAM write at guest address a (row 127 = dummy)
+// keep the HRAM fetch mirror in step with a RAM write at guest address a (row PK_HC_ROWS = dummy)
 __device__ __forceinline__ void hcode_st(const Ctx& c, u32 a, u32 v) {
-    const u32 row = sel(a - 0xFF80u < 0x7Fu, a - 0xFF80u, 0x7Fu);
+    const u32 row = sel(a - 0xFF80u < PK_HC_ROWS, a - 0xFF80u, PK_HC_ROWS);
     lds_hcode[row * PK_WG_ENVS + c.loc] = (u8)v;
 }
 
@@ -407,8 +411,8 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
     c.env = env;
     c.gid = __builtin_amdgcn_readfirstlane(env / PK_LANES);
     c.g = A.mem + (size_t)c.gid * PK_GROUP_STRIDE;
-    c.loc = (threadIdx.x >> 6) * A.wave_lanes + wl;  // < PK_WG_ENVS: <= 256 envs per workgroup
-    for (u32 i = 0; i < 0x7Fu; i++) lds_hcode[i * PK_WG_ENVS + c.loc] = (u8)ld_img(c, PK_P_HRAM + i);
+    c.loc = (threadIdx.x >> 6) * A.wave_lanes + wl;  // < PK_WG_ENVS envs per workgroup
+    for (u32 i = 0; i < PK_HC_ROWS; i++) lds_hcode[i * PK_WG_ENVS + c.loc] = (u8)ld_img(c, PK_P_HRAM + i);
 
     const u32 np = A.npad;
     u32* R = A.regs;
@@ -498,7 +502,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             // code outside the staged ROM (rare): RAM code such as the HRAM OAM-DMA wait loop reads the
             // image (three loads when pc..pc+2 stay in one 512-byte block of plain RAM), else the bus
             if (PK_RARE(exec & !flds)) {
-                if (pc - 0xFF80u < 0x7Du) {  // pc..pc+2 inside HRAM: the LDS mirror
+                if (pc - 0xFF80u < PK_HC_ROWS - 2u) {  // pc..pc+2 inside the mirrored HRAM bytes
                     const u32 q = (pc - 0xFF80u) * PK_WG_ENVS + c.loc;
                     bytes = lds_hcode[q] | (lds_hcode[q + PK_WG_ENVS] << 8) | (lds_hcode[q + 2u * PK_WG_ENVS] << 16);
                     ev |= PK_EV_F_BUS | PK_EV_HRAM;
@@ -716,7 +720,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             const u32 la = sel(fl, rom_lds_index(s, npc), 0u);
             // staged ROM and the HRAM code mirror are read together, unconditionally (one LDS round
             // trip; a lane whose pc is not in HRAM reads mirror row 0 and discards it)
-            const bool fh = npc - 0xFF80u < 0x7Du;
+            const bool fh = npc - 0xFF80u < PK_HC_ROWS - 2u;
             const u32 q = sel(fh, npc - 0xFF80u, 0u) * PK_WG_ENVS + c.loc;
             const u32 r0 = romw[la >> 2], r1 = romw[(la >> 2) + 1u];
             const u32 h0 = lds_hcode[q], h1 = lds_hcode[q + PK_WG_ENVS], h2 = lds_hcode[q + 2u * PK_WG_ENVS];
@@ -915,7 +919,7 @@ hipError_t pk_launch_step(const PkStepArgs& a, hipStream_t s) {
     const u32 wl = a.wave_lanes;
     const u32 span = ((a.env1 + PK_LANES - 1u) & ~(PK_LANES - 1u)) - a.env0;
     const u32 threads = span * (PK_LANES / wl);
-    const u32 wide = 256u * PK_LANES / wl < PK_K1_MAX_THREADS ? 256u * PK_LANES / wl : PK_K1_MAX_THREADS;
+    const u32 wide = PK_WG_ENVS * PK_LANES / wl < PK_K1_MAX_THREADS ? PK_WG_ENVS * PK_LANES / wl : PK_K1_MAX_THREADS;
     const u32 block = a.block ? a.block : (threads / PK_LANES <= a.simds ? 256u : wide);
     const u32 grid = (threads + block - 1) / block;
     hipLaunchKernelGGL(pk_step_kernel, dim3(grid), dim3(block), 0, s, a);

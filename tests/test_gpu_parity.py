@@ -95,14 +95,16 @@ def test_game_rom_parity_wave_shapes(lanes, monkeypatch):
 
 @pytest.mark.parametrize("seed", [-1, 0, 3, 21, 47])
 @pytest.mark.parametrize("render", [True, False])
-def test_fuzz_rom_parity_512_thread_workgroups(seed, render, monkeypatch):
-    """The benchmarked K1 shape at small n: 512-thread workgroups (PK_K1_BLOCK), 32 envs per wave,
-    8 waves sharing the workgroup's HRAM mirror (columns up to 255); rendered and headless."""
+@pytest.mark.parametrize("lanes", ["32", "64"])
+def test_fuzz_rom_parity_512_thread_workgroups(seed, render, lanes, monkeypatch):
+    """The benchmarked K1 shapes at small n: 512-thread workgroups (PK_K1_BLOCK), 8 waves sharing
+    the workgroup's HRAM mirror — 32 envs per wave (configs[2]'s 65,536-env launch: columns up to
+    255) and 64 (launches of >= 131,072 envs: columns up to 511); rendered and headless."""
     monkeypatch.setenv("PK_K1_BLOCK", "512")
-    monkeypatch.setenv("PK_WAVE_LANES", "32")
+    monkeypatch.setenv("PK_WAVE_LANES", lanes)
     from pokegym_amd.testrom.game import game_rom
     rom = game_rom() if seed < 0 else fuzz_rom(seed)
-    n, steps = 256, 8
+    n, steps = (256 if lanes == "32" else 1024), 8
     gpu, ref = _run_both(rom, None, n, steps, 100 + seed, render=render)
     g = np.frombuffer(b"".join(gpu), np.uint8).reshape(n, -1)
     a = oracle.state_digests(g, headless=not render)
@@ -134,3 +136,18 @@ def test_game_rom_64_banks_parity(render):
     b = oracle.state_digests(ref, headless=not render)
     bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in np.nonzero(a != b)[0][:4]]
     assert not bad, bad
+
+
+@pytest.mark.parametrize("shape", [("", ""), ("512", "32"), ("512", "64")])
+def test_hram_code_parity(shape, monkeypatch):
+    """Code run from inside, across and outside the HRAM bytes K1 mirrors in LDS (0xFF80-0xFF9F),
+    self-modified every pass, under the default shape and 512-thread workgroups of 32/64-env waves."""
+    from pokegym_amd.testrom.fuzz import hram_code_rom
+    block, lanes = shape
+    if block:
+        monkeypatch.setenv("PK_K1_BLOCK", block)
+        monkeypatch.setenv("PK_WAVE_LANES", lanes)
+    n = 1024 if lanes == "64" else 256
+    gpu, ref = _run_both(hram_code_rom(), None, n, 4, 31)
+    bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
+    assert not bad, bad[:4]

@@ -43,3 +43,9 @@ def test_hostsim_fuzz_64_banks(seed):
 def test_hostsim_game_64_banks():
     """pkbench on the 64-bank layout (overworld engine in 60 banks behind Bankswitch trampolines)."""
     assert check(game_rom(64), 8, 8, 5) == []
+
+
+def test_hostsim_hram_code():
+    """Code fetched from inside, across and outside the LDS-mirrored HRAM bytes, self-modified."""
+    from pokegym_amd.testrom.fuzz import hram_code_rom
+    assert check(hram_code_rom(), 8, 3, 5) == []
