@@ -560,6 +560,23 @@ static uint32_t k1_wave_lanes(const pk_handle* h, uint32_t count) {
     return npad / 64u >= 2u * h->simds ? 64u : 32u;
 }
 
+// K1 wave shape and workgroup size of a launch.  A sub-batch range is shaped as if every env of the
+// handle were resident at once: VecEnv steps its sub-batches concurrently on their own streams, and
+// K1 runs one workgroup per CU (LDS), so concurrent ranges share the GPU only when each is laid
+// out for its part of the CUs — e.g. the two 65,536-env halves of a 131,072-env handle run as 64-env
+// waves in 512-thread workgroups, 128 CUs each, two waves per SIMD overall (shaped alone, each
+// took every CU and the second range waited: 485k vs 688k env-steps/s).
+static void k1_shape(const pk_handle* h, uint32_t& lanes, uint32_t& block) {
+    lanes = k1_wave_lanes(h, h->n);
+    if (h->k1_block) {
+        block = h->k1_block;
+        return;
+    }
+    const uint32_t waves = ((h->n + PK_LANES - 1u) / PK_LANES) * (PK_LANES / lanes);
+    const uint32_t wide = PK_WG_ENVS * PK_LANES / lanes < PK_K1_MAX_THREADS ? PK_WG_ENVS * PK_LANES / lanes : PK_K1_MAX_THREADS;
+    block = waves <= h->simds ? 256u : wide;
+}
+
 static PkStepArgs step_args(pk_handle* h, const uint8_t* actions, uint32_t env0, uint32_t env1) {
     PkStepArgs a;
     memset(&a, 0, sizeof a);
@@ -569,9 +586,8 @@ static PkStepArgs step_args(pk_handle* h, const uint8_t* actions, uint32_t env0,
     a.release_frame = h->release; a.render_last = (h->flags & PK_F_RENDER) ? 1 : 0;
     a.lat_stride = (uint32_t)h->lat_stride;
     a.nslots = h->nslots; a.bank_slot = h->bank_slot; a.slot_bank = h->slot_bank;
-    a.wave_lanes = k1_wave_lanes(h, env1 - env0);
+    k1_shape(h, a.wave_lanes, a.block);
     a.simds = h->simds;
-    a.block = h->k1_block;
     a.dbg = h->dbg;
     a.env0 = env0; a.env1 = env1;
     return a;

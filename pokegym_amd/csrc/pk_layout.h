@@ -61,6 +61,12 @@ enum {
     PK_NREGS
 };
 
+// largest K1 workgroup (one per CU: its envs share one LDS copy of the ROM banks and microcode):
+// 512 threads = 8 waves, two per SIMD at 221 VGPRs; at most PK_WG_ENVS envs (HRAM code mirror columns)
+#ifndef PK_K1_MAX_THREADS
+#define PK_K1_MAX_THREADS 512
+#endif
+#define PK_WG_ENVS 512u
 #define PK_LDS_SLOTS 6u  // ROM banks (16 KiB each) staged in LDS by the step kernel (slot 0 = bank 0)
 
 // kernel argument blocks (passed by value)

@@ -34,11 +34,7 @@
 #define CPU_QUEUED 4u
 #define CPU_CRASH 8u
 #define PK_NO_BANK 0xFFFFFFFFu
-// largest K1 workgroup (one per CU: its envs share one LDS copy of the ROM banks and microcode):
-// 512 threads = 8 waves, two per SIMD at 221 VGPRs
-#ifndef PK_K1_MAX_THREADS
-#define PK_K1_MAX_THREADS 512
-#endif
+
 
 // debug hooks: the host-simulation build (tests/hostsim) records an instruction trace and
 // per-iteration event bits; the gfx950 build compiles them away.
@@ -83,7 +79,6 @@ __shared__ int8_t lds_slot[128];                                                
 // stay on the image (authoritative); every HRAM write also updates the mirror (lanes that do not
 // write a mirrored byte store to the dummy row, so the store needs no branch).  Up to 512 envs per
 // workgroup: 64-env waves two per SIMD when a launch has the envs for it (>= 131,072).
-#define PK_WG_ENVS 512u
 #define PK_HC_ROWS 32u
 __shared__ u8 lds_hcode[(PK_HC_ROWS + 1u) * PK_WG_ENVS];
 
