@@ -8,5 +8,8 @@ mkdir -p $OUT
 cd $R
 PK_BENCH_REHEARSAL=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
     --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 4 --warmup 1 --envs 8192 \
-    > $OUT/n2.json 2> $OUT/n2.err
+    > $OUT/n2.json 2> $OUT/n2.err && \
+PK_BENCH_REHEARSAL=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --steps 3 --warmup 1 \
+    > $OUT/n2_default.json 2> $OUT/n2_default.err
 echo "exit=$?" > $OUT/exit.txt
