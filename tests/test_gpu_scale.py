@@ -62,6 +62,33 @@ def test_config3_geometry_65536_envs():
         emu.close()
 
 
+def test_capacity_geometry_131072_envs_sub_batches():
+    """131,072 envs in two concurrent 65,536-env sub-batches (pk_step_range on two streams): the
+    shape of configs[3] split over two GPUs — 64-env waves, 512-env workgroups, two waves per SIMD
+    across the two launches, HRAM mirror columns up to 511 — every env vs the oracle."""
+    import torch
+    from pokegym_amd.emulator import BatchedEmulator
+    from pokegym_amd.testrom.game import game_rom
+    rom, n, steps, half = game_rom(), 131072, 1, 65536
+    actions = np.random.default_rng(131072).integers(0, 9, (steps, n), dtype=np.uint8)
+    with OP.pool() as ex:
+        futs = OP.batch_digests(ex, rom, None, actions, chunk=2048)
+        emu = BatchedEmulator(rom, n, render=True)
+        acts = torch.from_numpy(actions).to(emu.device)
+        streams = [torch.cuda.Stream() for _ in range(2)]
+        cur = torch.cuda.current_stream()
+        for t in range(steps):
+            for b in (1, 0):
+                streams[b].wait_stream(cur)
+                with torch.cuda.stream(streams[b]):
+                    emu.step_range(b * half, acts[t, b * half:(b + 1) * half])
+            for st in streams:
+                cur.wait_stream(st)
+        torch.cuda.synchronize()
+        _check_states(rom, None, actions, emu, futs, headless=False)
+        emu.close()
+
+
 def test_config2_geometry_4096_envs_headless_cycle():
     """configs[1]: 4,096 envs, no PPU render (LCD folding + HALT skip-ahead paths), the fixed
     [0,3,1,2] cycle (half the envs at a per-env phase, half with random presses incl. none)."""
