@@ -184,3 +184,24 @@ def test_config4_shard_vecenv_sub_batches():
     assert np.array_equal(gpu_digests(full.emu), gpu_digests(sub.emu))
     full.close()
     sub.close()
+
+
+def test_512_env_workgroups_48_steps(monkeypatch):
+    """The >= 131,072-env K1 shape (64-env waves in 512-thread workgroups, HRAM mirror columns up
+    to 511) over 48 env-steps of pkbench, 1,024 envs, every env vs the oracle."""
+    import torch
+    from pokegym_amd.emulator import BatchedEmulator
+    from pokegym_amd.testrom.game import game_rom
+    monkeypatch.setenv("PK_K1_BLOCK", "512")
+    monkeypatch.setenv("PK_WAVE_LANES", "64")
+    rom, n, steps = game_rom(), 1024, 48
+    actions = np.random.default_rng(512).integers(0, 9, (steps, n), dtype=np.uint8)
+    with OP.pool() as ex:
+        futs = OP.batch_digests(ex, rom, None, actions, chunk=64)
+        emu = BatchedEmulator(rom, n, render=True)
+        acts = torch.from_numpy(actions).to(emu.device)
+        for t in range(steps):
+            emu.step(acts[t])
+        torch.cuda.synchronize()
+        _check_states(rom, None, actions, emu, futs, headless=False)
+        emu.close()
