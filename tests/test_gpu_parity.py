@@ -114,11 +114,15 @@ def test_fuzz_rom_parity_512_thread_workgroups(seed, render, lanes, monkeypatch)
 
 
 @pytest.mark.parametrize("seed", [2, 13, 40])
-def test_fuzz_rom_parity_64_banks(seed):
+@pytest.mark.parametrize("lanes", ["", "64"])
+def test_fuzz_rom_parity_64_banks(seed, lanes, monkeypatch):
     """1 MiB fuzz cartridges: code and data in the 58 switchable banks K1 does not stage in LDS
-    (global-ROM fetch and read paths)."""
+    (global-ROM fetch and read paths); also under 512-thread workgroups of 64-env waves."""
+    if lanes:
+        monkeypatch.setenv("PK_K1_BLOCK", "512")
+        monkeypatch.setenv("PK_WAVE_LANES", lanes)
     rom = fuzz_rom(seed, n_banks=64)
-    n, steps = 128, 12
+    n, steps = (128 if not lanes else 512), 12
     gpu, ref = _run_both(rom, None, n, steps, 200 + seed)
     bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
     assert not bad, bad[:4]
