@@ -124,6 +124,10 @@ def main():
     ap.add_argument("--rom-banks", type=int, default=4, help="pkbench size in 16 KiB banks (4, or 64 = 1 MiB)")
     ap.add_argument("--state", default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-obs", action="store_true",
+                    help="diagnostic: also hand every step's observation to the host (pinned buffers, D2H on a "
+                         "copy stream overlapped with the next step) inside the timed region -- the PCIe-inclusive "
+                         "rate of a numpy-consuming caller (DESIGN.md section 6); not the default bench line")
     args = ap.parse_args()
 
     import torch
@@ -207,6 +211,32 @@ def main():
             if world > 1 and t % 128 == 127:
                 dist.all_reduce(stats)
 
+    host_copy = None
+    if args.host_obs:
+        if vec is not None:
+            raise SystemExit("--host-obs: not for the VecEnv workload (its consumer is on the device)")
+        src = emu.obs if reward else emu.screen
+        dbuf = [torch.empty_like(src) for _ in range(2)]
+        hbuf = [torch.empty(src.shape, dtype=src.dtype, pin_memory=True) for _ in range(2)]
+        cstream = torch.cuda.Stream(dev)
+        cdone = [None, None]
+
+        def host_copy(t):
+            # compute stream: snapshot the obs into a device double buffer (HBM copy, ~0.5 ms), then
+            # the copy stream moves it over PCIe while the next step runs
+            k = t % 2
+            cur = torch.cuda.current_stream(dev)
+            if cdone[k] is not None:
+                cur.wait_event(cdone[k])   # this buffer's previous D2H has finished
+            dbuf[k].copy_(emu.obs if reward else emu.screen)
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            cstream.wait_event(ev)
+            with torch.cuda.stream(cstream):
+                hbuf[k].copy_(dbuf[k], non_blocking=True)
+                cdone[k] = torch.cuda.Event()
+                cdone[k].record(cstream)
+
     total = args.warmup + args.steps
     mode = args.actions if args.actions != "auto" else W["actions"]
     g = torch.Generator(device=dev)
@@ -222,6 +252,8 @@ def main():
 
     for t in range(args.warmup):
         env_step(t, False)
+        if host_copy:
+            host_copy(t)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -231,6 +263,8 @@ def main():
     t0 = time.perf_counter()
     for t in range(args.warmup, total):
         env_step(t, True)
+        if host_copy:
+            host_copy(t)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -283,6 +317,8 @@ def main():
                 "release_frame": 8,
                 "max_episode_steps": max_steps,
                 "parallelism": f"envs sharded over {world} GPU(s), no data-path collective",
+                "host_obs": ("every step's obs copied to pinned host memory inside the timed region (PCIe-inclusive; "
+                             "diagnostic, not the default line)") if args.host_obs else None,
                 "scaling_note": ("the default workload is configs[2] (config3: 65,536 envs on one GPU) at N=1 and "
                                  "configs[3] itself (config4: 262,144 envs split over the N GPUs, strong scaling) at "
                                  "N>1.  A GPU's rate depends on its env count — 32,768 envs: ~279k env-steps/s, "
