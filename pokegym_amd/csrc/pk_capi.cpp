@@ -225,6 +225,7 @@ struct pk_handle {
     uint32_t wave_lanes = 0;   // envs per wave in K1: 0 = by launch size (k1_wave_lanes), else PK_WAVE_LANES
     uint32_t simds = 1024;     // SIMDs of the device (4 per CU)
     uint32_t k1_block = 0;     // K1 workgroup size override (PK_K1_BLOCK), 0 = by geometry
+    int k1_prio = -1;          // K1 wave-priority variant override (PK_K1_PRIO 0/1), -1 = by shape
     uint32_t frames = 24, release = 8, flags = 0, max_steps = 20480;
     uint32_t mbc = 3, bank_mask = 0;
     uint8_t* mem = nullptr;
@@ -347,6 +348,7 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
             }
             h->k1_block = (uint32_t)v;
         }
+        if (const char* pr = getenv("PK_K1_PRIO")) h->k1_prio = atoi(pr) ? 1 : 0;
     }
     h->frames = cfg->frame_skip;
     h->release = cfg->release_frame;
@@ -566,15 +568,18 @@ static uint32_t k1_wave_lanes(const pk_handle* h, uint32_t count) {
 // out for its part of the CUs — e.g. the two 65,536-env halves of a 131,072-env handle run as 64-env
 // waves in 512-thread workgroups, 128 CUs each, two waves per SIMD overall (shaped alone, each
 // took every CU and the second range waited: 485k vs 688k env-steps/s).
-static void k1_shape(const pk_handle* h, uint32_t& lanes, uint32_t& block) {
+// The wide (512-thread) shape puts two waves on each SIMD; those launches take K1's wave-priority
+// variant (measured +5 % at 65,536 envs; with one wave per SIMD it only costs its two instructions).
+static void k1_shape(const pk_handle* h, uint32_t& lanes, uint32_t& block, uint32_t& prio) {
     lanes = k1_wave_lanes(h, h->n);
     if (h->k1_block) {
         block = h->k1_block;
-        return;
+    } else {
+        const uint32_t waves = ((h->n + PK_LANES - 1u) / PK_LANES) * (PK_LANES / lanes);
+        const uint32_t wide = PK_WG_ENVS * PK_LANES / lanes < PK_K1_MAX_THREADS ? PK_WG_ENVS * PK_LANES / lanes : PK_K1_MAX_THREADS;
+        block = waves <= h->simds ? 256u : wide;
     }
-    const uint32_t waves = ((h->n + PK_LANES - 1u) / PK_LANES) * (PK_LANES / lanes);
-    const uint32_t wide = PK_WG_ENVS * PK_LANES / lanes < PK_K1_MAX_THREADS ? PK_WG_ENVS * PK_LANES / lanes : PK_K1_MAX_THREADS;
-    block = waves <= h->simds ? 256u : wide;
+    prio = h->k1_prio >= 0 ? (uint32_t)h->k1_prio : (block > 256u ? 1u : 0u);
 }
 
 static PkStepArgs step_args(pk_handle* h, const uint8_t* actions, uint32_t env0, uint32_t env1) {
@@ -586,7 +591,7 @@ static PkStepArgs step_args(pk_handle* h, const uint8_t* actions, uint32_t env0,
     a.release_frame = h->release; a.render_last = (h->flags & PK_F_RENDER) ? 1 : 0;
     a.lat_stride = (uint32_t)h->lat_stride;
     a.nslots = h->nslots; a.bank_slot = h->bank_slot; a.slot_bank = h->slot_bank;
-    k1_shape(h, a.wave_lanes, a.block);
+    k1_shape(h, a.wave_lanes, a.block, a.prio);
     a.simds = h->simds;
     a.dbg = h->dbg;
     a.env0 = env0; a.env1 = env1;

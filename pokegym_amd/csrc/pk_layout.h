@@ -92,6 +92,7 @@ struct PkStepArgs {
     uint32_t wave_lanes;      // envs per 64-lane wave in K1 (64, 32 or 16): fewer lanes = more waves/SIMD
     uint32_t simds;           // SIMDs of the device: K1 uses 256-thread workgroups while waves <= simds
     uint32_t block;           // K1 workgroup size override (0 = by geometry; PK_K1_BLOCK, tests)
+    uint32_t prio;            // K1 wave-priority variant (two waves per SIMD; PK_K1_PRIO overrides)
     unsigned long long* dbg;  // diagnostic counters (-DPK_STAMP builds only), else null
     uint32_t env0, env1;      // env range of this launch: [env0, env1), env0 % 64 == 0 (sub-batches)
 };

@@ -377,6 +377,9 @@ __device__ __forceinline__ void pk_write_slow(const PkStepArgs* A, u8* g, u32 la
 
 // ---------------------------------------------------------------------------------------------
 // K1
+// PRIO: the launch runs two waves per SIMD (A.prio, chosen by the host), and K1 raises a wave's
+// issue priority over its dependent fetch -> decode -> operand-read chain (see the prefetch stage)
+template <bool PRIO>
 __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A) {
     for (u32 i = threadIdx.x; i < PK_UC_ENTRIES * PK_UE_WORDS; i += blockDim.x) lds_uc[i] = A.ucode[i];
     for (u32 i = threadIdx.x; i < 128u; i += blockDim.x) lds_slot[i] = A.bank_slot[i];
@@ -590,6 +593,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             }
             PK_STAMP_AT(1);
         }
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);   // operand read issued: the SIMD's other wave first
         const u32 m0 = rm0 | om0 | (xm & 0xFFu), m1 = rm1 | sel(rd2, om1, 0u) | (xm >> 8);
         ev |= sel(rd, PK_EV_RD | sel(rd2, PK_EV_RD2, 0u) | sel(rram, PK_EV_RD_RAM, 0u) | sel(rrom, PK_EV_RD_ROMLDS, 0u)
                       | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
@@ -709,6 +713,11 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
                       | sel(addr0 >= 0xC000u && addr0 < 0xFE00u, PK_EV_WR_WRAM, sel(addr0 >= 0x8000u && addr0 < 0xA000u, PK_EV_WR_VRAM, 0u)), 0u);
 
         // ---------------- prefetch the next instruction (LDS-staged ROM or the HRAM mirror) ----------------
+        // wave priority (two waves per SIMD): from here through the next iteration's fetch, decode
+        // and address to its operand read — a dependent chain of LDS and memory round trips — this
+        // wave wins issue over the SIMD's other wave, which is meanwhile in its (long, latency-free)
+        // datapath; the read is issued sooner and its latency overlaps the other wave's ALU work
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
         {
             const u32 npc = s.pc;
             const bool fl = rom_staged(s, npc) && (npc & 0x3FFFu) < 0x3FFEu;
@@ -917,6 +926,9 @@ hipError_t pk_launch_step(const PkStepArgs& a, hipStream_t s) {
     const u32 wide = PK_WG_ENVS * PK_LANES / wl < PK_K1_MAX_THREADS ? PK_WG_ENVS * PK_LANES / wl : PK_K1_MAX_THREADS;
     const u32 block = a.block ? a.block : (threads / PK_LANES <= a.simds ? 256u : wide);
     const u32 grid = (threads + block - 1) / block;
-    hipLaunchKernelGGL(pk_step_kernel, dim3(grid), dim3(block), 0, s, a);
+    if (a.prio)
+        hipLaunchKernelGGL(pk_step_kernel<true>, dim3(grid), dim3(block), 0, s, a);
+    else
+        hipLaunchKernelGGL(pk_step_kernel<false>, dim3(grid), dim3(block), 0, s, a);
     return hipGetLastError();
 }

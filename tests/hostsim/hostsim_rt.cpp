@@ -28,7 +28,7 @@ static void launch_independent(dim3 grid, dim3 block, const std::function<void()
 }
 
 void pk_sim_launch(const char* name, dim3 grid, dim3 block, const std::function<void()>& body) {
-    if (strcmp(name, "pk_step_kernel") != 0) {  // the only kernel with __shared__ + __syncthreads
+    if (strncmp(name, "pk_step_kernel", 14) != 0) {  // the only kernel with __shared__ + __syncthreads
         launch_independent(grid, block, body);
         return;
     }

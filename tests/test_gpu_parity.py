@@ -99,7 +99,8 @@ def test_game_rom_parity_wave_shapes(lanes, monkeypatch):
 def test_fuzz_rom_parity_512_thread_workgroups(seed, render, lanes, monkeypatch):
     """The benchmarked K1 shapes at small n: 512-thread workgroups (PK_K1_BLOCK), 8 waves sharing
     the workgroup's HRAM mirror — 32 envs per wave (configs[2]'s 65,536-env launch: columns up to
-    255) and 64 (launches of >= 131,072 envs: columns up to 511); rendered and headless."""
+    255) and 64 (launches of >= 131,072 envs: columns up to 511); rendered and headless.  The wide
+    shape also selects K1's wave-priority variant (pk_step_kernel<true>), as those launches do."""
     monkeypatch.setenv("PK_K1_BLOCK", "512")
     monkeypatch.setenv("PK_WAVE_LANES", lanes)
     from pokegym_amd.testrom.game import game_rom

@@ -12,13 +12,13 @@ def kernel_means(d, kernel="pk_step_kernel"):
     vals = defaultdict(lambda: defaultdict(float))
     for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
         for row in csv.DictReader(open(f)):
-            if not row["Kernel_Name"].startswith(kernel):
+            if kernel not in row["Kernel_Name"]:
                 continue
             vals[row["Dispatch_Id"]][row["Counter_Name"]] += float(row["Counter_Value"])
     durs = {}
     for f in glob.glob(os.path.join(d, "*kernel_trace.csv")):
         for row in csv.DictReader(open(f)):
-            if row["Kernel_Name"].startswith(kernel):
+            if kernel in row["Kernel_Name"]:
                 durs[row["Dispatch_Id"]] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9
     # the last dispatch of the run (steady state), counters summed over dimensions
     last = sorted(vals, key=int)[-1]

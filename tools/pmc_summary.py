@@ -11,7 +11,8 @@ def load(dirpath):
     agg = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(dirpath, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            k = row.get("Kernel_Name", "?").split("(")[0]
+            # "pk_render_kernel(...)", "void pk_step_kernel<true>(...)" -> the kernel's base name
+            k = row.get("Kernel_Name", "?").split("(")[0].split("<")[0].split(" ")[-1]
             agg[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
     return agg
 

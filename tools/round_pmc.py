@@ -18,7 +18,7 @@ def per_dispatch(d, kernel):
     vals = defaultdict(lambda: defaultdict(float))
     for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
         for row in csv.DictReader(open(f)):
-            if row["Kernel_Name"].startswith(kernel):
+            if kernel in row["Kernel_Name"]:
                 vals[int(row["Dispatch_Id"])][row["Counter_Name"]] += float(row["Counter_Value"])
     return vals
 
@@ -50,7 +50,7 @@ def main():
     k1 = []
     for fcsv in glob.glob(os.path.join(D, "stats", "*kernel_stats.csv")):
         for row in csv.DictReader(open(fcsv)):
-            if row["Name"].startswith("pk_step_kernel"):
+            if "pk_step_kernel" in row["Name"]:
                 k1.append(float(row["AverageNs"]) / 1e6)
     bench = json.loads(open(os.path.join(D, "stats_bench.json")).read().strip().splitlines()[-1])
     out = {
