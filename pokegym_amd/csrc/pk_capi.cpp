@@ -551,15 +551,21 @@ int pk_set_ram(pk_handle* h, uint16_t addr, uint32_t len, const uint8_t* dense, 
     return 0;
 }
 
-// K1 envs per wave for a launch of `count` envs (measured, profiles/r02_sweep_*): 32 until the
-// launch has two 64-lane waves per SIMD, then 64.  At 65,536 envs two 32-lane waves per SIMD beat
-// one 64-lane wave by ~10 %; at 32,768 one 32-lane wave per SIMD matches two 16-lane ones; below,
-// the launch is latency-bound and more, narrower waves do not help (4,096 envs at 4 per wave on
-// every CU measured 2.4x slower).  PK_WAVE_LANES fixes the shape.
+// K1 envs per wave for a launch of `count` envs (measured, profiles/r02_sweep_*, r02_ab/ab_prio.txt):
+// the widest wave that still gives two waves per SIMD, whose priority variant hides one wave's
+// fetch -> operand-read chain behind the other's datapath — 64 from 131,072 envs, 32 from 65,536
+// (two 32-lane waves per SIMD beat one 64-lane wave by ~10 %), 16 for (16,384, 32,768] (configs[3]'s
+// per-GPU shard: two 16-lane waves with priority +5 % over one 32-lane wave; without priority they
+// were 4 % slower).  Smaller launches are latency-bound and keep one 32-lane wave per SIMD (more,
+// narrower waves do not help: 4,096 envs at 4 per wave on every CU measured 2.4x slower); between
+// the thresholds the narrower shape would need a second round of workgroups.  PK_WAVE_LANES fixes it.
 static uint32_t k1_wave_lanes(const pk_handle* h, uint32_t count) {
     if (h->wave_lanes) return h->wave_lanes;
     const uint32_t npad = (count + PK_LANES - 1u) & ~(PK_LANES - 1u);
-    return npad / 64u >= 2u * h->simds ? 64u : 32u;
+    if (npad / 64u >= 2u * h->simds) return 64u;
+    if (npad / 32u >= 2u * h->simds) return 32u;
+    if (npad / 16u > h->simds && npad / 16u <= 2u * h->simds) return 16u;
+    return 32u;
 }
 
 // K1 wave shape and workgroup size of a launch.  A sub-batch range is shaped as if every env of the

@@ -95,17 +95,18 @@ def test_game_rom_parity_wave_shapes(lanes, monkeypatch):
 
 @pytest.mark.parametrize("seed", [-1, 0, 3, 21, 47])
 @pytest.mark.parametrize("render", [True, False])
-@pytest.mark.parametrize("lanes", ["32", "64"])
+@pytest.mark.parametrize("lanes", ["16", "32", "64"])
 def test_fuzz_rom_parity_512_thread_workgroups(seed, render, lanes, monkeypatch):
     """The benchmarked K1 shapes at small n: 512-thread workgroups (PK_K1_BLOCK), 8 waves sharing
-    the workgroup's HRAM mirror — 32 envs per wave (configs[2]'s 65,536-env launch: columns up to
-    255) and 64 (launches of >= 131,072 envs: columns up to 511); rendered and headless.  The wide
+    the workgroup's HRAM mirror — 16 envs per wave (configs[3]'s 32,768-env shard: columns up to
+    127), 32 (configs[2]'s 65,536-env launch: columns up to 255) and 64 (launches of >= 131,072
+    envs: columns up to 511); rendered and headless.  The wide
     shape also selects K1's wave-priority variant (pk_step_kernel<true>), as those launches do."""
     monkeypatch.setenv("PK_K1_BLOCK", "512")
     monkeypatch.setenv("PK_WAVE_LANES", lanes)
     from pokegym_amd.testrom.game import game_rom
     rom = game_rom() if seed < 0 else fuzz_rom(seed)
-    n, steps = (256 if lanes == "32" else 1024), 8
+    n, steps = {"16": 256, "32": 256, "64": 1024}[lanes], 8
     gpu, ref = _run_both(rom, None, n, steps, 100 + seed, render=render)
     g = np.frombuffer(b"".join(gpu), np.uint8).reshape(n, -1)
     a = oracle.state_digests(g, headless=not render)
