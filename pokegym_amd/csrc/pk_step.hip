@@ -662,6 +662,9 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             // IME / HALT / CRASH / QUEUED: (cpu & keep) | set from the microcode
             s.cpu = (s.cpu & (0xFFFFFFF0u | ((K >> PK_KB_CPUAND) & 15u))) | (K >> PK_KB_CPUOR);
         }
+        // priority 2 from here (the writes and the next instruction's address): above a wave in its
+        // datapath (0), below one in its fetch -> operand-read chain (3)
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(2);
         // next instruction in an unstaged switchable bank (most of a 64-bank cartridge): its two
         // global-ROM dwords are requested now, so their latency overlaps the write stage (a lane
         // whose write switches the ROM bank refetches at the top of the next iteration)
