@@ -321,9 +321,9 @@ def main():
                              "diagnostic, not the default line)") if args.host_obs else None,
                 "scaling_note": ("the default workload is configs[2] (config3: 65,536 envs on one GPU) at N=1 and "
                                  "configs[3] itself (config4: 262,144 envs split over the N GPUs, strong scaling) at "
-                                 "N>1.  A GPU's rate depends on its env count — 32,768 envs: ~300k env-steps/s, "
-                                 "65,536: ~475k, 131,072: ~700k (one launch needs 64 envs per SIMD to hide its "
-                                 "latency and 128 to fill every lane; profiles/r02k, profiles/r02q) — so N=8 "
+                                 "N>1.  A GPU's rate depends on its env count — 32,768 envs: ~305k env-steps/s, "
+                                 "65,536: ~490k, 131,072: ~720k (one launch needs 64 envs per SIMD to hide its "
+                                 "latency and 128 to fill every lane; profiles/r02r/envs) — so N=8 "
                                  "(32,768 per GPU) is below 8x the N=1 rate by construction of configs[3]"),
             },
             "roofline": {
