@@ -53,40 +53,84 @@ WORKLOADS = {
 }
 
 
-def _cpu_baseline(rom: bytes, state, seconds_target: float = 12.0):
-    """The oracle (C restatement of the path, oracle/gbcore.c) on the host cores: "port"."""
+def _cpu_quota():
+    """The host CPU share this process may use: the cgroup CPU quota (cgroup v2 cpu.max or v1
+    cfs_quota/period) when one is set, else None; plus the raw values for the record."""
+    raw = None
+    try:
+        raw = open("/sys/fs/cgroup/cpu.max").read().strip()
+        q, p = raw.split()[:2]
+        if q != "max":
+            return max(1, int(-(-int(q) // int(p)))), f"cpu.max {raw}"
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            raw = f"cfs_quota_us {q} / cfs_period_us {p}"
+            if q > 0:
+                return max(1, -(-q // p)), raw
+        except (OSError, ValueError):
+            pass
+    return None, raw
+
+
+def _cpu_run(rom, state, workers, n_per, steps, seed0):
+    """workers forked processes, each n_per envs x steps timed env-steps (after 3 warmup) of the C
+    oracle; aggregate env-steps/s over the slowest process's timed span."""
     import multiprocessing as mp
     from oracle import oracle
-    oracle.lib()
-    workers = int(os.environ.get("PK_CPU_BASELINE_PROCS", "16"))
-    # calibrate: one short single-thread run sizes the per-worker sample to ~seconds_target/2
-    sec, _ = oracle.bench(rom, state, 2, 3, 4, 99)
-    per_step = sec / 8.0
-    steps = max(4, int(seconds_target / 2.0 / per_step / 4))
-    n_per = 4
     ctx = mp.get_context("fork")
     with ctx.Pool(workers) as pool:
         t0 = time.time()
-        res = pool.starmap(oracle.bench, [(rom, state, n_per, 3, steps, 1000 + w) for w in range(workers)])
+        res = pool.starmap(oracle.bench, [(rom, state, n_per, 3, steps, seed0 + w) for w in range(workers)])
         wall = time.time() - t0
-    total_steps = workers * n_per * steps
     slowest = max(r[0] for r in res)
+    return workers * n_per * steps / slowest, wall, sum(r[1] for r in res) / slowest
+
+
+def _cpu_baseline(rom: bytes, state, seconds_target: float = 10.0):
+    """The oracle (C restatement of the path, oracle/gbcore.c) on the host cores: "port".
+
+    Main value: the reference's own CPU shape, 72 envs each in its own worker process
+    (README.md:116-118; PufferLib multiprocessing), on whatever cores the box grants.  Beside it, a
+    run sized to the box's CPU share (cgroup quota, else the 16 threads the GPU box allots one GPU:
+    OMP_NUM_THREADS) with 4 envs per process, and the workload intensity of the same action stream."""
+    from oracle import oracle
+    oracle.lib()
     try:
         affinity = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        affinity = None
+        affinity = os.cpu_count()
+    quota, quota_raw = _cpu_quota()
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    share = quota or omp or 16
+    share = max(1, min(share, affinity or share))
+    # calibrate: seconds per env-step of one process
+    sec, _ = oracle.bench(rom, state, 2, 3, 4, 99)
+    per_step = sec / 8.0
+    # 72 processes x 1 env on `share` cores: ~seconds_target of wall
+    steps72 = max(4, int(seconds_target * share / 72 / per_step))
+    v72, wall72, ips72 = _cpu_run(rom, state, 72, 1, steps72, 2000)
+    steps_s = max(4, int(seconds_target / 4 / per_step))
+    vs, walls, _ = _cpu_run(rom, state, share, 4, steps_s, 1000)
+    inten = oracle.intensity(rom, state, 8, 3, 4, 99)
     return {
-        "value": round(total_steps / slowest, 1),
+        "value": round(v72, 1),
         "unit": "env-steps/s",
-        "cores": workers,
-        "host_cpus": os.cpu_count(),
-        "affinity_cpus": affinity,
+        "cores": min(72, share),
         "kind": "port",
-        "sample": (f"{workers} worker processes (the box's CPU share; os.cpu_count() = {os.cpu_count()} is the whole "
-                   f"machine) x {n_per} envs x {steps} timed env-steps (after 3 warmup) of the same ROM on the C "
-                   f"oracle (oracle/gbcore.c, 1 thread/process, random actions); aggregate over the slowest "
-                   f"process's timed span; pool wall {wall:.1f}s; PyBoy+pokegym itself is not installed"),
-        "instr_per_s": round(sum(r[1] for r in res) / slowest, 1),
+        "sample": (f"the reference's CPU shape: 72 envs, one per worker process (README.md:116-118), x {steps72} timed "
+                   f"env-steps each (after 3 warmup) of the same ROM and random actions on the C oracle "
+                   f"(oracle/gbcore.c, 1 thread/process), on a CPU share of {share} cores "
+                   f"({'cgroup ' + quota_raw if quota else 'no cgroup quota; OMP_NUM_THREADS=' + str(omp or 'unset') + ' is the box share'}); "
+                   f"aggregate over the slowest process's timed span; pool wall {wall72:.1f}s. PyBoy+pokegym itself is "
+                   "not installed (pure-Python PyBoy would be slower than this C restatement)"),
+        "instr_per_s": round(ips72, 1),
+        "cpu_share": {"cores": share, "cgroup": quota_raw, "omp_num_threads": omp or None, "affinity_cpus": affinity,
+                      "host_cpus": os.cpu_count()},
+        "share_sized_run": {"value": round(vs, 1), "procs": share, "envs_per_proc": 4, "steps": steps_s,
+                            "pool_wall_s": round(walls, 1)},
+        "workload_intensity": {k: round(v, 4) for k, v in inten.items()},
     }
 
 
@@ -165,14 +209,17 @@ def main():
 
     # N>1: configs[3]/[4] themselves, their 262,144 envs split over the ranks (strong scaling)
     strong = world > 1 and args.envs is None and wname in ("config4", "config5")
+    log_every = max(1, min(128, args.steps))
     n = args.envs or ((CONFIGS3_ENVS // world) & ~63 if strong else W["envs"])
     reward = W["reward"]
     max_steps = args.max_episode_steps or (16 if reward else 20480)
     vec = None
     if W["vecenv"]:
         from pokegym_amd.env import VecEnv
+        # logging interval min(128, steps): the episode-stat all-reduce (RCCL at N>1) and the
+        # sticky-error check fire inside the timed steps (any `steps` consecutive env-steps hold one)
         vec = VecEnv(n, rom=rom, state=state, power_on=state is None, device=local, reward=False,
-                     max_episode_steps=max_steps, log_interval=128, batch_size=n // args.batches)
+                     max_episode_steps=max_steps, log_interval=log_every, batch_size=n // args.batches)
         emu = vec.emu
         vec.async_reset()
     else:
@@ -184,6 +231,7 @@ def main():
     stats = torch.zeros(3, dtype=torch.float64, device=dev)  # [sum of episodic returns, episodes, resets]
     rst = [torch.cuda.Event(enable_timing=True) for _ in range(2 * (args.warmup + args.steps))]
     rst_i = [0]
+    ar_ev = []   # (start, end) events around each timed all-reduce (config5 at N>1)
 
     def env_step(t, timed):
         if vec is not None:
@@ -208,8 +256,15 @@ def main():
             if timed:
                 rst[rst_i[0] + 1].record()
                 rst_i[0] += 2
-            if world > 1 and t % 128 == 127:
+            if world > 1 and t % log_every == log_every - 1:
+                # configs[4]'s episodic-return all-reduce (RCCL), every min(128, steps) env-steps
+                evs = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if timed else None
+                if timed:
+                    evs[0].record()
                 dist.all_reduce(stats)
+                if timed:
+                    evs[1].record()
+                    ar_ev.append(evs)
 
     host_copy = None
     if args.host_obs:
@@ -273,6 +328,9 @@ def main():
     instr = emu.last_instr_count()  # last step's emulated instructions (all envs)
     resets = float(stats[1].item()) - resets0
     k5_ms = sum(rst[2 * i].elapsed_time(rst[2 * i + 1]) for i in range(rst_i[0] // 2))
+    ar_ms = [a.elapsed_time(b) for a, b in ar_ev]
+    # env-steps t (1-based) inside the timed window at which the logging interval fires
+    fired = sum(1 for t in range(args.warmup + 1, total + 1) if t % log_every == 0)
     t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -328,6 +386,10 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
+                "measured_bound": ("issue + dependent latency (not HBM, not MFMA): per emulated SM83 instruction a wave "
+                                   "issues the fetch -> decode -> address -> operand-read chain and a ~100-instruction "
+                                   "VALU datapath; `issue` below carries the PMC figures and `frac` is only the HBM "
+                                   "price of the algorithmic bytes (DESIGN.md section 5)"),
                 "kernel": ("pk_step_kernel (K1, 24 emulated frames) + pk_render_kernel (K2)"
                            + (" + pk_reward_kernel/pk_obs_kernel (K4/K3)" if reward else "")),
                 "span": ("sum of the step's kernel times per launch (HIP events on the launch stream, averaged "
@@ -353,6 +415,16 @@ def main():
         if stamp:
             out["pmc_stamp"] = {k: stamp[k] for k in ("valu_busy_pct", "valu_utilization_pct", "wait_any_pct",
                                                       "waves_per_simd", "source") if k in stamp}
+            if "issue" in stamp:
+                out["roofline"]["issue"] = stamp["issue"]
+        out["collectives"] = {
+            "interval_env_steps": log_every,
+            "fired_in_timed_steps": fired if (vec is not None or reward) else 0,
+            "what": ("VecEnv logging: sticky-error check + episode/info statistics all-reduce (RCCL at N>1)"
+                     if vec is not None else "episodic-return all-reduce of configs[4] (RCCL at N>1)" if reward else None),
+            "allreduce_ms": [round(x, 3) for x in ar_ms] if ar_ms else None,
+            "note": None if world > 1 else "one rank: the all-reduce is an identity and is not issued",
+        }
         if reward:
             out["resets"] = {"envs_reset": int(resets), "k5_reset_ms_total": round(k5_ms, 3),
                              "k5_reset_ms_per_step": round(k5_ms / max(args.steps, 1), 3)}

@@ -55,6 +55,7 @@ struct gb {
     /* header bytes 1..4 of the state file */
     uint8_t hdr[4];
     uint64_t instr_count, frame_count, iter_count;
+    uint64_t cyc_total, cyc_halted, cyc_lcdoff;   /* workload intensity (gb_intensity) */
 };
 
 static const uint32_t TIMER_DIVIDERS[4] = {1024, 16, 64, 256};
@@ -774,6 +775,9 @@ void gb_tick(gb_t* gb) {
         gb->IF |= lcd_tick(gb, (uint32_t)cycles);
         budget += (uint32_t)cycles + 1u;
         gb->iter_count++;
+        gb->cyc_total += cycles;
+        if (gb->halted) gb->cyc_halted += cycles;
+        if (!(gb->LCDC & 0x80)) gb->cyc_lcdoff += cycles;
         if (budget > PK_FRAME_BUDGET) gb->frame_done = 1;
     } while (!gb->frame_done);
     gb->frame_done = 0;
@@ -991,4 +995,29 @@ double gb_bench(const uint8_t* rom, uint32_t rom_len, const uint8_t* state, uint
     gb_free(tmpl);
     if (instr_out) *instr_out = i1 - i0;
     return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+}
+
+/* Workload intensity of the bench's action stream (the same actions as gb_bench): out[0] emulated
+ * instructions, [1] ticks, [2] cycles, [3] cycles spent halted (HALT fast-forward), [4] cycles with
+ * the LCD off, [5] frames — summed over n envs x steps env-steps after warmup. */
+int gb_intensity(const uint8_t* rom, uint32_t rom_len, const uint8_t* state, uint32_t state_len,
+                 uint32_t n, uint32_t warmup, uint32_t steps, uint32_t seed, uint64_t* out) {
+    gb_t* tmpl = gb_new(rom, rom_len);
+    if (!tmpl) return -1;
+    if (state && gb_load_state(tmpl, state, state_len)) { gb_free(tmpl); return -2; }
+    for (int k = 0; k < 6; k++) out[k] = 0;
+    #define ACT(e, t) ((int)((((uint64_t)(seed) * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)(e) * 0xBF58476D1CE4E5B9ull) ^ ((uint64_t)(t) * 0x94D049BB133111EBull)) >> 61))
+    for (uint32_t e = 0; e < n; e++) {
+        gb_t* g = gb_clone(tmpl);
+        for (uint32_t t = 0; t < warmup; t++) gb_run_action(g, ACT(e, t), 24, 8);
+        const uint64_t i0 = g->instr_count, k0 = g->iter_count, c0 = g->cyc_total, h0 = g->cyc_halted,
+                       l0 = g->cyc_lcdoff, f0 = g->frame_count;
+        for (uint32_t t = warmup; t < warmup + steps; t++) gb_run_action(g, ACT(e, t), 24, 8);
+        out[0] += g->instr_count - i0; out[1] += g->iter_count - k0; out[2] += g->cyc_total - c0;
+        out[3] += g->cyc_halted - h0; out[4] += g->cyc_lcdoff - l0; out[5] += g->frame_count - f0;
+        gb_free(g);
+    }
+    #undef ACT
+    gb_free(tmpl);
+    return 0;
 }

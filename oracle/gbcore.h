@@ -81,6 +81,8 @@ int gb_batch_run(const uint8_t* rom, uint32_t rom_len, const uint8_t* state, uin
                  uint8_t* states_out /* n*v9 or NULL */, uint8_t* screens_out /* n*144*160 or NULL */);
 
 /* CPU baseline timing (single thread); returns seconds of the timed part. */
+int gb_intensity(const uint8_t* rom, uint32_t rom_len, const uint8_t* state, uint32_t state_len,
+                 uint32_t n, uint32_t warmup, uint32_t steps, uint32_t seed, uint64_t* out);
 double gb_bench(const uint8_t* rom, uint32_t rom_len, const uint8_t* state, uint32_t state_len,
                 uint32_t n, uint32_t warmup, uint32_t steps, uint32_t seed, uint64_t* instr_out);
 

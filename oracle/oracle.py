@@ -168,6 +168,24 @@ def batch_run(rom: bytes, state: bytes | None, actions: np.ndarray, want_states=
     return so, sc
 
 
+def intensity(rom: bytes, state: bytes | None, n: int, warmup: int, steps: int, seed: int) -> dict:
+    """Workload intensity of gb_bench's action stream (oracle/gbcore.c gb_intensity)."""
+    r = np.frombuffer(rom, dtype=np.uint8).copy()
+    st = np.frombuffer(state, dtype=np.uint8).copy() if state is not None else None
+    out = np.zeros(6, np.uint64)
+    L = lib()
+    L.gb_intensity.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                               ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+    rc = L.gb_intensity(_ptr(r), len(r), _ptr(st) if st is not None else None, len(st) if st is not None else 0,
+                        n, warmup, steps, seed, out.ctypes.data)
+    if rc:
+        raise ValueError(f"gb_intensity failed: {rc}")
+    instr, ticks, cyc, halted, lcdoff, frames = (int(x) for x in out)
+    return {"instr_per_env_step": instr / (n * steps), "ticks_per_env_step": ticks / (n * steps),
+            "halted_frac": halted / max(cyc, 1), "lcd_off_frac": lcdoff / max(cyc, 1),
+            "busy_cycles_per_frame": (cyc - halted) / max(frames, 1), "cycles_per_frame": cyc / max(frames, 1)}
+
+
 def bench(rom: bytes, state: bytes | None, n: int, warmup: int, steps: int, seed: int):
     """Single-thread CPU timing of the oracle: returns (seconds, emulated_instructions)."""
     r = np.frombuffer(rom, dtype=np.uint8).copy()

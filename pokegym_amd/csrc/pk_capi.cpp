@@ -34,6 +34,8 @@ hipError_t pk_launch_reward(const PkRewardArgs& a, hipStream_t s);
 hipError_t pk_launch_rreset_pre(const PkRewardArgs& a, hipStream_t s);
 hipError_t pk_launch_rreset_post(const PkRewardArgs& a, hipStream_t s);
 hipError_t pk_launch_obs(const PkRewardArgs& a, hipStream_t s);
+hipError_t pk_launch_seen_rehash(const uint32_t* old_tab, uint32_t old_lg, uint32_t* new_tab, uint32_t new_lg,
+                                 const uint32_t* rs, uint32_t n, uint32_t np, hipStream_t s);
 hipError_t pk_launch_ram_copy(uint8_t* mem, uint8_t* dense, uint32_t n, uint32_t phys0, uint32_t len,
                               uint32_t to_dense, hipStream_t s);
 
@@ -344,7 +346,7 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
             int v = atoi(bl);
             if (v < 64 || v > 512 || (v % 64) || (uint32_t)(v / 64) * (h->wave_lanes ? h->wave_lanes : 32u) > 512u) {
                 delete h;
-                return fail(-EINVAL, "PK_K1_BLOCK must be a multiple of 64 in [64, 512] with (block/64)*wave_lanes <= 256");
+                return fail(-EINVAL, "PK_K1_BLOCK must be a multiple of 64 in [64, 512] with (block/64)*wave_lanes <= 512");
             }
             h->k1_block = (uint32_t)v;
         }
@@ -381,7 +383,7 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     ALLOC(h->lat, 3 * h->lat_stride * 4);
     ALLOC(h->screen, (size_t)h->npad * PK_SCREEN);
     ALLOC(h->rom, cfg->rom_len + 16);
-    ALLOC(h->ucode, PK_UC_ENTRIES * PK_UE_WORDS * 4);
+    ALLOC(h->ucode, PK_UC_WORDS * 4);
     ALLOC(h->bank_slot, 128);
     ALLOC(h->slot_bank, PK_LDS_SLOTS);
     ALLOC(h->t_mem, PK_PHYS);
@@ -408,7 +410,7 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
         if (h->flags & PK_F_HEATMAP) ALLOC(h->heat, (size_t)h->npad * PK_HEAT_ROWS * PK_HEAT_COLS * 4);
     }
 #undef ALLOC
-    std::vector<uint32_t> uc(PK_UC_ENTRIES * PK_UE_WORDS);
+    std::vector<uint32_t> uc(PK_UC_WORDS);
     pk_build_ucode(uc.data());
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = hipMemset(h->rom + cfg->rom_len, 0xFF, 16);
@@ -579,7 +581,10 @@ static uint32_t k1_wave_lanes(const pk_handle* h, uint32_t count) {
 static void k1_shape(const pk_handle* h, uint32_t& lanes, uint32_t& block, uint32_t& prio) {
     lanes = k1_wave_lanes(h, h->n);
     if (h->k1_block) {
+        // PK_K1_BLOCK with the lanes picked for this handle: a workgroup holds at most PK_WG_ENVS
+        // envs (its HRAM code mirror), so a block too large for 64-lane waves is narrowed
         block = h->k1_block;
+        if ((block / PK_LANES) * lanes > PK_WG_ENVS) block = PK_WG_ENVS / lanes * PK_LANES;
     } else {
         const uint32_t waves = ((h->n + PK_LANES - 1u) / PK_LANES) * (PK_LANES / lanes);
         const uint32_t wide = PK_WG_ENVS * PK_LANES / lanes < PK_K1_MAX_THREADS ? PK_WG_ENVS * PK_LANES / lanes : PK_K1_MAX_THREADS;
@@ -875,8 +880,9 @@ int pk_profile_read(pk_handle* h, double* emu_ms, double* render_ms, double* rew
 }
 
 // Environment.reset(max_episode_steps, reward_scale) (environment.py:1233, :1258-1259): the episode
-// length and reward scale of the following steps.  The seen-coordinate set grows (and restarts
-// empty) when the new episode length needs more capacity; call it before the reset it belongs to.
+// length and reward scale of the following steps.  When the new episode length needs a larger
+// seen-coordinate set, every env's current-episode entries are re-inserted into the larger table
+// (pk_seen_rehash_kernel), so envs that are not reset keep their seen coordinates.
 int pk_set_episode_params(pk_handle* h, uint32_t max_episode_steps, double reward_scale) {
     if (!h) return fail(-EINVAL, "null handle");
     if (max_episode_steps == 0) return fail(-EINVAL, "max_episode_steps must be > 0");
@@ -890,6 +896,9 @@ int pk_set_episode_params(pk_handle* h, uint32_t max_episode_steps, double rewar
             const size_t bytes = (size_t)h->npad * (1ull << need) * 4;
             if (hipMalloc((void**)&seen, bytes) != hipSuccess) return fail(-ENOMEM, "hipMalloc(%zu) for the seen set", bytes);
             if (hipMemset(seen, 0, bytes) != hipSuccess) { (void)hipFree(seen); return fail(-EIO, "hipMemset failed"); }
+            hipError_t e = pk_launch_seen_rehash(h->seen, h->cap_log2, seen, need, h->rs, h->n, h->npad, nullptr);
+            if (e == hipSuccess) e = hipDeviceSynchronize();
+            if (e != hipSuccess) { (void)hipFree(seen); return fail(-EIO, "seen-set rehash: %s", hipGetErrorString(e)); }
             (void)hipFree(h->seen);
             h->seen = seen;
             h->cap_log2 = need;

@@ -732,7 +732,28 @@ __global__ void __launch_bounds__(256) pk_ram_copy_kernel(uint8_t* mem, uint8_t*
     }
 }
 
+// seen set grown by pk_set_episode_params: every env's entries of its current episode (tag ==
+// rs[RS_GEN]) re-inserted into the larger table (the new table is zeroed: older tags are dropped)
+__global__ void pk_seen_rehash_kernel(const u32* old_tab, u32 old_lg, u32* new_tab, u32 new_lg, const u32* rs, u32 n, u32 np) {
+    const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const u32 gen = rs[RS_GEN * np + e];
+    const u32* src = old_tab + (size_t)e * (1u << old_lg);
+    u32* dst = new_tab + (size_t)e * (1u << new_lg);
+    u32 count = 0;
+    for (u32 i = 0; i < (1u << old_lg); i++) {
+        const u32 v = src[i];
+        if (gen != 0u && (v >> 24) == gen) count += seen_insert(dst, new_lg, gen, v & 0xFFFFFFu, count) & 1u;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
+hipError_t pk_launch_seen_rehash(const u32* old_tab, u32 old_lg, u32* new_tab, u32 new_lg, const u32* rs, u32 n, u32 np,
+                                 hipStream_t s) {
+    hipLaunchKernelGGL(pk_seen_rehash_kernel, dim3((n + 255) / 256), dim3(256), 0, s, old_tab, old_lg, new_tab, new_lg, rs, n, np);
+    return hipGetLastError();
+}
+
 hipError_t pk_launch_reward(const PkRewardArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(pk_reward_kernel, dim3((a.env1 - a.env0 + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();

@@ -44,6 +44,9 @@
 #ifndef PK_ITER
 #define PK_ITER(env, ev) ((void)(ev))
 #endif
+#ifndef PK_ITER_OP
+#define PK_ITER_OP(env, di) ((void)0)
+#endif
 // diagnostic build only (-DPK_STAMP, tools/stamp_build.py): per-phase wave cycles of the loop,
 // read with s_memtime at points where the loop already waits, summed per wave into A.dbg
 #ifdef PK_STAMP
@@ -68,7 +71,7 @@ enum {
 };
 
 // LDS, staged by each workgroup at kernel entry
-__shared__ __attribute__((aligned(16))) u32 lds_uc[PK_UC_ENTRIES * PK_UE_WORDS];  // microcode
+__shared__ __attribute__((aligned(16))) u32 lds_uc[PK_UC_WORDS];                  // microcode + secondary ops
 __shared__ __attribute__((aligned(16))) u8 lds_rom[PK_LDS_SLOTS * 0x4000u + 16u]; // ROM banks (+ fetch overrun pad)
 __shared__ int8_t lds_slot[128];                                                  // bank -> slot
 // Fetch-only mirror of the first PK_HC_ROWS bytes of HRAM (0xFF80-0xFF9F: where games put the
@@ -381,7 +384,7 @@ __device__ __forceinline__ void pk_write_slow(const PkStepArgs* A, u8* g, u32 la
 // issue priority over its dependent fetch -> decode -> operand-read chain (see the prefetch stage)
 template <bool PRIO>
 __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A) {
-    for (u32 i = threadIdx.x; i < PK_UC_ENTRIES * PK_UE_WORDS; i += blockDim.x) lds_uc[i] = A.ucode[i];
+    for (u32 i = threadIdx.x; i < PK_UC_WORDS; i += blockDim.x) lds_uc[i] = A.ucode[i];
     for (u32 i = threadIdx.x; i < 128u; i += blockDim.x) lds_slot[i] = A.bank_slot[i];
     for (u32 sl = 0; sl < A.nslots; sl++) {
         const uint4* src = reinterpret_cast<const uint4*>(A.rom + (size_t)A.slot_bank[sl] * 0x4000u);
@@ -452,6 +455,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
     // flush_lines, K2's blank-screen path — clears its flag)
     s.render = (A.render_last && frame + 1u == A.frames) ? 1u : 0u;
     const uint4* ucv = reinterpret_cast<const uint4*>(lds_uc);
+    const uint4* ucv2 = reinterpret_cast<const uint4*>(lds_uc + PK_UC_U2);
     const u32* romw = reinterpret_cast<const u32*>(lds_rom);
 
     u32 budget = 0;  // frame watchdog (oracle/gbcore.c PK_FRAME_BUDGET)
@@ -662,6 +666,44 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             // IME / HALT / CRASH / QUEUED: (cpu & keep) | set from the microcode
             s.cpu = (s.cpu & (0xFFFFFFF0u | ((K >> PK_KB_CPUAND) & 15u))) | (K >> PK_KB_CPUOR);
         }
+        // ---------------- fused secondary op (pk_ucode.h pk_u2_entry) ----------------
+        // The instruction after this one, if it is a JR (cc), LD r,r', INC/DEC BC/DE/HL or NOP, runs
+        // in this iteration on the registers and flags just written, as PyBoy's next cpu.tick would,
+        // when nothing could happen between the two: this instruction may fuse (PK_DB_FUSE: executed,
+        // no control transfer / IME / HALT / DAA), its cycles raise no LCD event or frame end (clock
+        // stays below the LCD target, or below the frame length with the LCD off) and no watchdog end,
+        // the timer is off (no TIMA overflow), it writes no IO/MBC register (slow write) and, when the
+        // code runs from RAM, nothing at all (the prefetched bytes stay valid).  Its bytes are among
+        // the 4 fetched ones (3 when the code is outside the ROM or within 3 bytes of a bank end) and
+        // none of them is an IO register (DIV and a folded STAT change with the clock).
+        const bool wr = bit(D, PK_DB_WR) != 0u && taken != 0u, wr2 = bit(D, PK_DB_WR2) != 0u;
+        const bool wram = wr & fast01;
+        {
+            const u32 nxt = bytes >> (8u * (D & 3u));
+            const uint4 u2 = ucv2[nxt & 0xFFu];
+            const u32 M2 = u2.y;
+            const u32 len2 = (M2 >> PK_U2B_LEN) & 3u;
+            const bool nb4 = (pc < 0x8000u) & ((pc & 0x3FFFu) <= 0x3FFCu);
+            const u32 lim = sel(s.lcd0 & 0x80u, s.target, FRAME_CYCLES);
+            const bool fuse = (bit(D, PK_DB_FUSE) != 0u) & ((M2 & 3u) != 0u) & ((D & 3u) + len2 <= sel(nb4, 4u, 3u))
+                            & (s.clock + cycles < lim) & (budget + cycles + 1u <= 16u * FRAME_CYCLES) & !(s.tim0 & (4u << 24))
+                            & !(wr & (!wram | (pc >= 0x8000u))) & !(pc - 0xFEFEu < 0x82u);
+            // register ops: val2 = pair +- 1 (bytes 0-1) or the source register (byte 3), written back
+            // through the entry's selectors; JR: condition on the new F, target pc + 2 + e
+            const u32 v2 = perm(s.w1, s.w0, u2.x) + (u32)sfield(M2, PK_U2B_DELTA, 8);
+            const u32 w0f = perm(v2, s.w0, u2.z), w1f = perm(v2, s.w1, u2.w);
+            const u32 tk2 = ((((w1f >> 16) | 0x100u) >> ((M2 >> PK_U2B_CPOS) & 15u)) & 1u) ^ bit(M2, PK_U2B_CINV);
+            const bool jr2 = (M2 & 3u) == PK_U2_JR;
+            const u32 pc2 = (s.pc + len2 + sel(jr2 & (tk2 != 0u), (u32)(int)(int8_t)(u8)(nxt >> 8), 0u)) & 0xFFFFu;
+            if (fuse) PK_TRACE(env, s.pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, nxt & 0xFFu);
+            s.w0 = sel(fuse, w0f, s.w0);
+            s.w1 = sel(fuse, w1f, s.w1);
+            s.pc = sel(fuse, pc2, s.pc);
+            cycles += sel(fuse, ((M2 >> PK_U2B_CYC) & 15u) * 4u + sel(jr2 & (tk2 != 0u), 4u, 0u), 0u);
+            budget += sel(fuse, 1u, 0u);
+            icount += sel(fuse, 1u, 0u);
+        }
+
         // priority 2 from here (the writes and the next instruction's address): above a wave in its
         // datapath (0), below one in its fetch -> operand-read chain (3)
         if constexpr (PRIO) __builtin_amdgcn_s_setprio(2);
@@ -678,12 +720,10 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         }
 
         // ---------------- memory writes (wv0 at addr0, wv1 at addr1) ----------------
-        const bool wr = bit(D, PK_DB_WR) != 0u && taken != 0u, wr2 = bit(D, PK_DB_WR2) != 0u;
         const u32 pushv = sel(bit(U, PK_UB_WPC), pcn, sel(bit(U, PK_UB_WSP), sp, Y & 0xFFFFu));
         const u32 wv = sel(bit(U, PK_UB_W16), pushv, res8);
         const bool hifirst = bit(D, PK_DB_ADIR + 1) != 0u;  // adir = -1: push writes the high byte first
         const u32 wv0 = sel(hifirst, wv >> 8, wv) & 0xFFu, wv1 = sel(hifirst, wv, wv >> 8) & 0xFFu;
-        const bool wram = wr & fast01;
         if (wram) {
             // VRAM / OAM change while rendered lines are pending: rasterise them first (rare)
             // (lines are pending only in the rendered frame: test that first, alone)
@@ -880,6 +920,8 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         budget += cycles + 1u;
         ev |= sel(s.frame_done != 0u || budget > 16u * FRAME_CYCLES, PK_EV_FRAME, 0u);
         PK_ITER(env, ev);
+        PK_ITER_OP(env, sel(exec, sel((bytes & 0xFFu) == 0xCBu, 256u + b1, bytes & 0xFFu),
+                            sel(dispatch, PK_UC_INT, sel(doint, PK_UC_NOP0, PK_UC_IDLE))));
         if (PK_RARE((s.frame_done != 0u) | (budget > 16u * FRAME_CYCLES))) {  // frame end or watchdog
             s.frame_done = 0;
             budget = 0;

@@ -25,6 +25,10 @@ enum { PK_UE_D = 0, PK_UE_U, PK_UE_K, PK_UE_V, PK_UE_XR, PK_UE_XE, PK_UE_YR, PK_
 #define PK_UC_INT 512u    // pseudo-op: interrupt dispatch (push PC, jump to the vector)
 #define PK_UC_IDLE 513u   // pseudo-op: halted / crashed CPU, 4 cycles
 #define PK_UC_NOP0 514u   // pseudo-op: interrupt pending with IME off (queued), 0 cycles
+// secondary-op table (fused pairs, see pk_u2_entry): 256 entries x 4 dwords after the main table
+#define PK_U2_WORDS 4u
+#define PK_UC_U2 (PK_UC_ENTRIES * PK_UE_WORDS)
+#define PK_UC_WORDS (PK_UC_U2 + 256u * PK_U2_WORDS)
 
 // D word: memory, timing, control
 #define PK_DB_LEN 0       // 2 bits  instruction length
@@ -33,6 +37,7 @@ enum { PK_UE_D = 0, PK_UE_U, PK_UE_K, PK_UE_V, PK_UE_XR, PK_UE_XE, PK_UE_YR, PK_
 #define PK_DB_WR 4        // write wv0 at addr0
 #define PK_DB_WR2 5       // write wv1 at addr1
 #define PK_DB_ASP 6       // (builder only) address source SP        -> AE selector
+#define PK_DB_FUSE 6      // (stored word) a secondary op may follow in the same iteration (pk_u2_entry)
 #define PK_DB_AIMM 7      // (builder only) address source immediate -> AE selector
 #define PK_DB_AHN 8       // (builder only) immediate address 0xFF00|n
 #define PK_DB_AOFF 9      // 2 bits signed: addr0 = src + aoff
@@ -456,6 +461,11 @@ static inline void pk_store_uop(uint32_t* e, PkUop o, bool real) {
     if (o.d & pk_fld(1, PK_DB_ASP)) ae = PK_E_SP;
     else if (o.d & pk_fld(1, PK_DB_AIMM)) ae = (o.d & pk_fld(1, PK_DB_AHN)) ? PK_E_HN : PK_E_NN;
     e[PK_UE_D] = o.d & ~(pk_fld(1, PK_DB_ASP) | pk_fld(1, PK_DB_AIMM) | pk_fld(1, PK_DB_AHN) | pk_fld(1, PK_DB_YSP));
+    // a secondary op may be fused after this one: executed instructions without control transfer,
+    // IME/HALT/STOP changes or the rare DAA path (pk_u2_entry states the remaining conditions)
+    if (real && ts == PK_T_NONE && !(o.d & (pk_fld(3, PK_DB_IME) | pk_fld(1, PK_DB_HALT) | pk_fld(1, PK_DB_CRASH) |
+                                            pk_fld(1, PK_DB_DAA))) && (o.d & 3u) != 0u)
+        e[PK_UE_D] |= pk_fld(1, PK_DB_FUSE);
     e[PK_UE_U] = o.u & ~63u;
     e[PK_UE_K] = o.k;
     // V word: datapath selectors derived from U in the form the kernel consumes in one op
@@ -473,7 +483,54 @@ static inline void pk_store_uop(uint32_t* e, PkUop o, bool real) {
     e[PK_UE_S1] = o.s1;
 }
 
-static inline void pk_build_ucode(uint32_t* t /* PK_UC_ENTRIES * PK_UE_WORDS */) {
+// ---- secondary ops: fused into the iteration of the instruction before them ----
+// The SIMT loop pays for one iteration per emulated instruction whatever the instruction, so the
+// cheap register-only successors of an instruction run in the same iteration: a JR (cc), LD r,r',
+// INC/DEC BC/DE/HL or NOP right after a fusable instruction (PK_DB_FUSE) executes on the registers
+// and flags that instruction left, exactly as the next cpu.tick would, when nothing can happen in
+// between — the instruction raised no LCD event, timer overflow or frame end, wrote no IO/IE/IF/MBC
+// register and no RAM code (pk_step.hip states the test).  Entry: x = val2 selector over w1:w0,
+// y = misc (class, length, cycles, condition, delta), z/w = writeback selectors (as S0/S1).
+enum { PK_U2_NONE = 0, PK_U2_REG = 1, PK_U2_JR = 2 };
+#define PK_U2B_LEN 2      // 2 bits length
+#define PK_U2B_CYC 4      // 4 bits cycles/4 (JR: not taken)
+#define PK_U2B_CPOS 8     // 4 bits: JR condition = bit cpos of (F | 0x100) ...
+#define PK_U2B_CINV 12    //         ^ cinv
+#define PK_U2B_DELTA 16   // 8 bits signed: val2 = pair + delta (INC/DEC rr)
+static inline void pk_u2_entry(uint32_t* e, int op) {
+    uint32_t cls = PK_U2_NONE, len = 1, cyc = 4, cpos = 8, cinv = 0;
+    int delta = 0;
+    PkUop o = pk_uop_base(1, 4);
+    o.s1 = PK_S0_ID;   // identity writeback of both words (val2 has no flags byte), zero val2 source
+    uint32_t sel2 = PK_PZERO;
+    if (op == 0x00) {
+        cls = PK_U2_REG;
+    } else if (op >= 0x40 && op < 0x80 && op != 0x76 && (op & 7) != 6 && ((op >> 3) & 7) != 6) {  // LD r, r'
+        cls = PK_U2_REG;
+        sel2 = 0x000C0C0Cu | (pk_r8_byte(op & 7) << 24);   // r' -> val2 byte 3 (the result8 slot)
+        pk_wb_r8(o, (op >> 3) & 7);
+    } else if ((op & 0xC7) == 0x03 && ((op >> 4) & 3) != 3) {  // INC rr / DEC rr (BC DE HL)
+        const int p = (op >> 4) & 3;
+        cls = PK_U2_REG;
+        cyc = 8;
+        sel2 = pk_sel16(p);
+        delta = (op & 8) ? -1 : 1;
+        pk_wb_r16(o, p);
+    } else if (op == 0x18 || op == 0x20 || op == 0x28 || op == 0x30 || op == 0x38) {  // JR (cc,) e
+        static const uint32_t pos[4] = {7, 7, 4, 4}, inv[4] = {1, 0, 1, 0};
+        cls = PK_U2_JR;
+        len = 2;
+        cyc = 8;   // + 4 when taken
+        if (op != 0x18) { cpos = pos[(op >> 3) & 3]; cinv = inv[(op >> 3) & 3]; }
+    }
+    e[0] = sel2;
+    e[1] = cls | (len << PK_U2B_LEN) | ((cyc / 4u) << PK_U2B_CYC) | (cpos << PK_U2B_CPOS) | (cinv << PK_U2B_CINV)
+         | (((uint32_t)delta & 0xFFu) << PK_U2B_DELTA);
+    e[2] = o.s0;
+    e[3] = o.s1;
+}
+
+static inline void pk_build_ucode(uint32_t* t /* PK_UC_WORDS */) {
     for (int i = 0; i < 512; i++) {
         PkUop o = i < 256 ? pk_uop(i) : pk_uop_cb(i - 256);
         if (i == 0xCB) o = pk_uop_base(2, 8);  // never executed: the kernel indexes 256 + second byte
@@ -487,4 +544,5 @@ static inline void pk_build_ucode(uint32_t* t /* PK_UC_ENTRIES * PK_UE_WORDS */)
     PkUop idle = pk_uop_base(0, 4), nop0 = pk_uop_base(0, 0);
     const PkUop ps[3] = {it, idle, nop0};
     for (int j = 0; j < 3; j++) pk_store_uop(t + (size_t)(512 + j) * PK_UE_WORDS, ps[j], false);
+    for (int op = 0; op < 256; op++) pk_u2_entry(t + PK_UC_U2 + (size_t)op * PK_U2_WORDS, op);
 }

@@ -60,6 +60,7 @@ class Environment:
         rom = _read(rom_path)
         state = _read(state_path if state_path is not None else DEFAULT_STATE)
         self.max_episode_steps, self.reward_scale = max_episode_steps, reward_scale
+        self._default_episode = (int(max_episode_steps), float(reward_scale))   # reset()'s defaults
         self.emu = BatchedEmulator(rom, 1, state=state, device=device, render=True, reward=True,
                                    max_episode_steps=max_episode_steps, reward_scale=reward_scale, heatmap=True)
         self.observation_space = spaces.observation_space()
@@ -120,11 +121,12 @@ class Environment:
         self.emu.load_env(0, data)
 
     def reset(self, seed=None, options=None, max_episode_steps=None, reward_scale=None):
-        """environment.py:1233-1334 (seeding is not supported, as in the reference).  As there,
-        max_episode_steps / reward_scale apply from this reset on (:1258-1259); None keeps the
-        current values (the constructor's, 20480 / 4.0 by default — the reference's reset defaults)."""
-        mes = self.max_episode_steps if max_episode_steps is None else int(max_episode_steps)
-        rsc = self.reward_scale if reward_scale is None else float(reward_scale)
+        """environment.py:1233-1334 (seeding is not supported, as in the reference).  As there, every
+        reset sets max_episode_steps / reward_scale from its arguments (:1258-1259): an argument left
+        out takes its default — the constructor's value, 20480 / 4.0 unless given (the reference's
+        reset defaults) — so one reset(max_episode_steps=X) does not stick to later resets."""
+        mes = self._default_episode[0] if max_episode_steps is None else int(max_episode_steps)
+        rsc = self._default_episode[1] if reward_scale is None else float(reward_scale)
         if (mes, rsc) != (self.max_episode_steps, self.reward_scale):
             self.emu.set_episode_params(mes, rsc)
             self.max_episode_steps, self.reward_scale = mes, rsc
@@ -247,9 +249,19 @@ class VecEnv:
     def _logical(self, obs: torch.Tensor) -> torch.Tensor:
         return obs.index_select(0, self._phys) if self._padded else obs
 
+    def _join_streams(self):
+        """The current stream waits for every sub-batch stream (steps still in flight)."""
+        if self._streams:
+            cur = torch.cuda.current_stream(self.device)
+            for st in self._streams:
+                cur.wait_stream(st)
+
     def reset(self, seed=None, max_episode_steps=None, reward_scale=None):
         """Reset every env; max_episode_steps / reward_scale (Environment.reset's arguments,
-        environment.py:1233) apply to all envs from here on, None keeps the current values."""
+        environment.py:1233) apply to all envs from here on, None keeps the current values.  Unlike
+        the single Environment (where each reset() restores 20480 / 4.0, as the reference does), they
+        are the VecEnv's configuration: its device auto-resets keep them."""
+        self._join_streams()
         if max_episode_steps is not None or reward_scale is not None:
             mes = max_episode_steps if max_episode_steps is not None else getattr(self.emu, "max_episode_steps", 20480)
             rsc = reward_scale if reward_scale is not None else getattr(self.emu, "reward_scale", 4.0)
@@ -300,6 +312,10 @@ class VecEnv:
     def _log(self):
         infos = []
         if self.log_interval and self._batch_steps % (self.log_interval * self.num_batches) == 0:
+            # the sticky error codes and the statistics rows are written by the sub-batch streams:
+            # wait for every one of them before reading and clearing (the next send() orders its
+            # stream after these reads again through st.wait_stream(current))
+            self._join_streams()
             self.raise_if_failed()
             infos = [self.stats.allreduce()]
             if self.info_stats is not None:
@@ -311,6 +327,7 @@ class VecEnv:
         if isinstance(actions, np.ndarray):
             actions = torch.from_numpy(actions)
         a = actions.to(device=self.device, dtype=torch.uint8).contiguous()
+        self._join_streams()
         if self.num_batches == 1:
             obs, rewards, terminals, truncations = self._step_range(0, a)
         else:

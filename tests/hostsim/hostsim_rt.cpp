@@ -80,14 +80,26 @@ extern "C" uint64_t pk_sim_trace_get(uint32_t* out, uint64_t cap) {
 
 // ---- per-iteration event recording (PK_ITER) ----
 static std::vector<std::vector<uint32_t>> g_iter;
+static std::vector<std::vector<uint32_t>> g_iter_op;
 static bool g_iter_on = false;
 extern "C" void pk_sim_iter_enable(uint32_t n_envs, int on) {
     g_iter.assign(on ? n_envs : 0, {});
+    g_iter_op.assign(on ? n_envs : 0, {});
     g_iter_on = on != 0;
 }
 extern "C" void pk_sim_iter(uint32_t env, uint32_t ev) {
     if (!g_iter_on || env >= g_iter.size()) return;
     g_iter[env].push_back(ev);   // one env is stepped by one thread: no lock needed
+}
+extern "C" void pk_sim_iter_op(uint32_t env, uint32_t di) {
+    if (!g_iter_on || env >= g_iter_op.size()) return;
+    g_iter_op[env].push_back(di);
+}
+extern "C" uint64_t pk_sim_iter_op_get(uint32_t env, uint32_t* out, uint64_t cap) {
+    if (env >= g_iter_op.size()) return 0;
+    uint64_t n = g_iter_op[env].size();
+    if (out) memcpy(out, g_iter_op[env].data(), (n < cap ? n : cap) * 4);
+    return n;
 }
 extern "C" uint64_t pk_sim_iter_get(uint32_t env, uint32_t* out, uint64_t cap) {
     if (env >= g_iter.size()) return 0;

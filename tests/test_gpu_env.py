@@ -107,3 +107,46 @@ def test_environment_reset_takes_episode_params():
         assert not a.step(act)[2]
     a.close()
     b.close()
+
+
+@pytest.mark.gpu
+def test_environment_reset_params_do_not_stick():
+    """reset(max_episode_steps=X) then reset(): the reference resets both to their defaults on
+    every call (environment.py:1233, :1258-1259), so the second episode has the default length."""
+    from pokegym_amd.env import Environment
+    from pokegym_amd.testrom.game import game_rom
+    env = Environment(rom_path=game_rom())
+    env.reset(max_episode_steps=2, reward_scale=1.0)
+    assert not env.step(0)[2] and env.step(0)[2]
+    env.reset()
+    assert (env.max_episode_steps, env.reward_scale) == (20480, 4.0)
+    for _ in range(4):
+        assert not env.step(0)[2]
+    env.close()
+
+
+@pytest.mark.gpu
+def test_seen_set_growth_keeps_current_episode():
+    """pk_set_episode_params growing the seen-coordinate table re-inserts every env's entries of
+    its current episode: an env that is not reset keeps its exploration reward."""
+    import torch
+    from pokegym_amd.emulator import BatchedEmulator
+    from pokegym_amd.testrom.game import game_rom
+    emu = BatchedEmulator(game_rom(), 64, reward=True, max_episode_steps=100)
+    emu.reset()
+    g = torch.Generator(device=emu.device)
+    g.manual_seed(5)
+    acts = torch.randint(0, 8, (6, 64), generator=g, device=emu.device).to(torch.uint8)
+    ref = BatchedEmulator(game_rom(), 64, reward=True, max_episode_steps=100)
+    ref.reset()
+    for t in range(3):
+        emu.step(acts[t])
+        ref.step(acts[t])
+    emu.set_episode_params(100000, 4.0)       # grows the table; no reset follows
+    ref.set_episode_params(100, 4.0)
+    for t in range(3, 6):
+        _, ra, _, _ = emu.step(acts[t])
+        _, rb, _, _ = ref.step(acts[t])
+        assert torch.equal(ra, rb)
+    emu.close()
+    ref.close()

@@ -9,9 +9,8 @@ mkdir -p $O
 STEPS=${STEPS:-8}
 rc=0
 if [ -n "$PARITY" ]; then
-  for n in $LIBS; do
-    env PK_LIB=$R/pokegym_amd/lib/libpokegym_amd_$n.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "$PARITY" > $O/par_$n.log 2>&1 || { rc=$?; echo "exit=$rc" > $O/exit.txt; exit $rc; }
-  done
+  n=${LIBS%% *}
+  env PK_LIB=$R/pokegym_amd/lib/libpokegym_amd_$n.so timeout -k 10 600 python -u -m pytest ${PARITY_FILES:-tests/test_gpu_parity.py} -x -q --timeout 200 --timeout-method thread -k "$PARITY" > $O/par_$n.log 2>&1 || { rc=$?; echo "exit=$rc" > $O/exit.txt; exit $rc; }
 fi
 for rep in 1 2; do
   for w in $WLS; do
