@@ -66,7 +66,7 @@ enum {
     PK_EV_RD_ROMG = 1u << 8, PK_EV_RD_RAM = 1u << 9, PK_EV_RD_IO = 1u << 10, PK_EV_RD2 = 1u << 11,
     PK_EV_WR = 1u << 12, PK_EV_WR_SLOW = 1u << 13, PK_EV_WR2 = 1u << 14, PK_EV_LCD = 1u << 15,
     PK_EV_TIMER = 1u << 16, PK_EV_FRAME = 1u << 17, PK_EV_FLUSH = 1u << 18, PK_EV_HRAM = 1u << 19,
-    PK_EV_JUMP = 1u << 20, PK_EV_CB = 1u << 21, PK_EV_FAM0 = 1u << 22 /* 22..27: unused here */,
+    PK_EV_JUMP = 1u << 20, PK_EV_CB = 1u << 21, PK_EV_FUSE = 1u << 22 /* 23..27: unused here */,
     PK_EV_RD_WRAM = 1u << 28, PK_EV_WR_WRAM = 1u << 29, PK_EV_WR_VRAM = 1u << 30, PK_EV_WR_HI = 1u << 31
 };
 
@@ -369,12 +369,14 @@ __device__ __forceinline__ u32 pk_read_slow(const PkStepArgs* A, u8* g, u32 lane
     return m0 | (m1 << 8);
 }
 __device__ __forceinline__ void pk_write_slow(const PkStepArgs* A, u8* g, u32 lane, u32 loc, u32 env, u32 gid, St* sp,
-                                                  u32 a0, u32 v0, u32 a1, u32 v1, u32 two) {
+                                                  u32 a0, u32 v0, u32 a1, u32 v1, u32 two, u32 hifirst) {
     Ctx c;
     c.A = A; c.g = g; c.lane = lane; c.env = env; c.gid = gid; c.loc = loc;
     St s = *sp;
+    // a push writes SP-1 (high byte) before SP-2 (low byte), as PyBoy's push does
+    if (two && hifirst) bus_write_any(c, s, a1, v1);
     bus_write_any(c, s, a0, v0);
-    if (two) bus_write_any(c, s, a1, v1);
+    if (two && !hifirst) bus_write_any(c, s, a1, v1);
     *sp = s;
 }
 
@@ -458,12 +460,12 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
     const uint4* ucv2 = reinterpret_cast<const uint4*>(lds_uc + PK_UC_U2);
     const u32* romw = reinterpret_cast<const u32*>(lds_rom);
 
-    u32 budget = 0;  // frame watchdog (oracle/gbcore.c PK_FRAME_BUDGET)
+    int slack = (int)(16u * FRAME_CYCLES);  // frame watchdog: PK_FRAME_BUDGET - budget (oracle/gbcore.c)
     // software pipeline: the next instruction's bytes and microcode entry, loaded from LDS at the
     // end of the previous iteration (after its writes, so bank switches and HRAM code stores are
     // seen) while the timer/LCD work runs; pf = 0 -> fetch and decode at the top instead
     u32 pf = 0, pbytes = 0;
-    uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0, p2 = p0;
+    uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0, p2 = p0, p3 = p0;
 #ifdef PK_STAMP
     uint64_t st_acc[PK_NSTAMP] = {}, st_prev = __builtin_amdgcn_s_memtime(), st_iter = 0;
 #endif
@@ -495,7 +497,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
 
         // ---------------- fetch + microcode entry (prefetched, or here when pf = 0) ----------------
         u32 bytes = pbytes;
-        uint4 e0 = p0, e1 = p1, e2 = p2;
+        uint4 e0 = p0, e1 = p1, e2 = p2, e3 = p3;
         if (PK_RARE(!pf)) {
             PK_STAMP_AT(8);
             const bool flds = rom_staged(s, pc) && (pc & 0x3FFFu) < 0x3FFEu;
@@ -530,9 +532,10 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             const u32 di = sel(exec, sel(op == 0xCBu, 256u + ((bytes >> 8) & 0xFFu), op),
                                sel(dispatch, PK_UC_INT, sel(doint, PK_UC_NOP0, PK_UC_IDLE)));
             ev |= sel(exec, sel(flds, PK_EV_F_LDS, 0u), 0u);
-            e0 = ucv[di * 3u];
-            e1 = ucv[di * 3u + 1u];
-            e2 = ucv[di * 3u + 2u];
+            e0 = ucv[di * 4u];
+            e1 = ucv[di * 4u + 1u];
+            e2 = ucv[di * 4u + 2u];
+            e3 = ucv[di * 4u + 3u];
             PK_STAMP_AT(9);
         }
         icount += sel(exec, 1u, 0u);
@@ -540,14 +543,11 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             | sel(dispatch, PK_EV_INT, 0u) | sel(!exec && !dispatch, PK_EV_IDLE, 0u);
         if (exec) PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, bytes & 0xFFu);
         const u32 D = e0.x, U = e0.y, K = e0.z, V = e0.w, XR = e1.x, XE = e1.y, YR = e1.z, YE = e1.w, AR = e2.x, AE = e2.y,
-                  S0 = e2.z, S1 = e2.w;
+                  S0 = e2.z, S1 = e2.w, YC = e3.x, YX = e3.y, CW = e3.z, CI = e3.w;
 
         // ---------------- operands, condition, memory address ----------------
         const u32 w0 = s.w0, w1 = s.w1, sp = s.sp;
-        const u32 b1 = (bytes >> 8) & 0xFFu;
         const u32 F = (w1 >> 16) & 0xFFu;
-        const u32 fc = (F >> 4) & 1u;
-        const u32 hl = w1 & 0xFFFFu;
         const u32 pcn = (pc + (D & 3u)) & 0xFFFFu;
         const u32 taken = (((F | 0x100u) >> ((D >> PK_DB_CPOS) & 15u)) & 1u) ^ bit(D, PK_DB_CINV);
         // operand pools: registers (w1:w0) and ext (q1:q0) = instruction bytes, m0|m1 and SP
@@ -598,48 +598,37 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             PK_STAMP_AT(1);
         }
         if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);   // operand read issued: the SIMD's other wave first
-        const u32 m0 = rm0 | om0 | (xm & 0xFFu), m1 = rm1 | sel(rd2, om1, 0u) | (xm >> 8);
+        // m0 | m1 << 8 (m1 is only meaningful for two-byte reads: one-byte operands select m0 alone)
+        const u32 m16 = rm0 | om0 | xm | ((rm1 | om1) << 8);
         ev |= sel(rd, PK_EV_RD | sel(rd2, PK_EV_RD2, 0u) | sel(rram, PK_EV_RD_RAM, 0u) | sel(rrom, PK_EV_RD_ROMLDS, 0u)
                       | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
                       | sel(addr0 >= 0xC000u && addr0 < 0xFE00u, PK_EV_RD_WRAM, 0u), 0u);
-        const u32 m16 = m0 | (m1 << 8);
         PK_STAMP_AT(0);
 
         // ---------------- fused datapath ----------------
         const u32 q1 = m16 | (sp << 16);
         const u32 X = perm(w1, w0, XR) | perm(q1, bytes, XE);
-        const u32 Y = perm(w1, w0, YR) | perm(q1, bytes, YE) | (K & 0xFFu);
-        const u32 sx8 = (u32)(int)(int8_t)(u8)b1 & 0xFFFFu;
-        // adder: r = X + (sub ? ~Y : Y) + cin; carries into each bit = X ^ Y' ^ r
-        const u32 sub = bit(U, PK_UB_SUB);
-        const u32 Yx = Y ^ ((0u - sub) & 0xFFFFu);
-        const u32 r = X + Yx + (sub ^ (bit(U, PK_UB_USEC) & fc));
-        const u32 cv = X ^ Yx ^ r;
-        const u32 hsh = 4u + 8u * bit(U, PK_UB_HC16);
-        const u32 hf = ((cv >> hsh) & 1u) ^ sub;
-        const u32 cf = ((cv >> (hsh + 4u)) & 1u) ^ sub;
-        // logic: (X & Y) and/or (X ^ Y) under all-ones masks from the microcode (OR = both)
-        const u32 lres = ((X & Y) & (u32)sfield(V, PK_VB_LAND, 1)) | ((X ^ Y) & (u32)sfield(V, PK_VB_LXOR, 1));
-        // rotate / shift / swap
-        const u32 x8 = X & 0xFFu;
-        const bool rdir = bit(U, PK_UB_RDIR) != 0u;
-        const u32 b7 = x8 >> 7, rob = sel(rdir, x8 & 1u, b7);
-        // rotate-in bit: bit RBIN of [0, F.C, rotated-out, bit 7]
-        const u32 bin = ((fc << 1) | (rob << 2) | (b7 << 3)) >> ((U >> PK_UB_RBIN) & 3u) & 1u;
-        const u32 rsh = sel(rdir, (x8 >> 1) | (bin << 7), ((x8 << 1) | bin) & 0xFFu);
-        const u32 rot = sel(bit(U, PK_UB_SWAP), ((x8 >> 4) | (x8 << 4)) & 0xFFu, rsh);
-        // results
-        // result8: byte R8 of the pool [Y, adder, logic, rotate] (two v_perm + one shift)
-        const u32 pool = perm(r, Y, 0x0C0C0400u) | perm(rot, lres, 0x04000C0Cu);
-        u32 res8 = (pool >> (V & 31u)) & 0xFFu;
-        const u32 hl1 = (hl + (u32)sfield(U, PK_UB_HLINC, 2)) & 0xFFFFu;
-        const u32 res16 = sel(bit(U, PK_UB_R16HL), hl1, r & 0xFFFFu);
-        // flags: F' = (F & keep) | const | Z | H | C
-        // C: bit FC of [0, adder carry, rotated-out, !F.C]
-        const u32 cbit = ((cf << 1) | (rob << 2) | ((fc ^ 1u) << 3)) >> ((U >> PK_UB_FC) & 3u) & 1u;
-        u32 nf = (F & (K >> PK_KB_FKEEP)) | (K >> PK_KB_FCONST) | sel(bit(U, PK_UB_FZ) && res8 == 0u, 0x80u, 0u)
-               | ((bit(U, PK_UB_FH) & hf) << 5) | (cbit << 4);
-        nf = sel(bit(U, PK_UB_FPOP), m0 & 0xF0u, nf) & 0xFFu;
+        const u32 Y = perm(w1, w0, YR) | perm(q1, bytes, YE) | YC;
+        // carry-in of the adder, or the bit shifted in by the right-shift unit: bit CW of
+        // (X | F << 16) ^ CI (F.C at bit 20, X's bits 7/0, bit 16 = 0 for the constants)
+        const u32 cin = ((((X & 0xFFFFu) | (w1 & 0xFFFF0000u)) ^ CI) & CW) != 0u ? 1u : 0u;
+        // adder: r = X + Y ^ YX + cin (YX = 0x1FFFF subtracts); X ^ Y ^ r = the carry (borrow) into
+        // each bit.  Left rotates and shifts are X + X + (0 / F.C / bit 7): bit 8 is the carry out
+        const u32 r = X + (Y ^ YX) + cin;
+        const u32 cvx = X ^ Y ^ r;
+        // right-shift unit: RRC RRA RR SRA SRL ((X | in << 8 | X.0 << 9) >> 1: bit 8 = the bit
+        // shifted out) and SWAP ((X | X << 8) >> 4)
+        const bool swap = bit(U, PK_US_SWAP) != 0u, right = bit(U, PK_US_RIGHT) != 0u;
+        const u32 rs = (X | (sel(swap, X, cin | ((X & 1u) << 1)) << 8)) >> sel(swap, 4u, 1u);
+        // logic: (X & Y) and/or (X ^ Y) (OR = both); loads are 0xFF AND Y
+        const u32 lres = ((X & Y) & (u32)sfield(U, PK_US_LAND, 1)) | ((X ^ Y) & (u32)sfield(U, PK_US_LXOR, 1));
+        u32 res8 = sel(bit(U, PK_US_LOGIC), lres, sel(right, rs, r)) & 0xFFu;
+        // flags: F' = (F & FK) | ((Z | H | C | FC) & FM), H/C = carry bits 4/8 (12/16 for ADD HL) or
+        // the right unit's shifted-out bit 8
+        const u32 cs = sel(right, rs, cvx) >> (bit(U, PK_US_HSH8) * 8u);
+        const u32 fv = sel(res8 == 0u, 0x80u, 0u) | ((cs << 1) & 0x20u) | ((cs >> 4) & 0x10u) | K;
+        u32 nf = ((F & (K >> 8)) | (fv & (K >> 16))) & 0xFFu;
+        nf = sel(bit(U, PK_US_FPOP), m16 & 0xF0u, nf);
         if (PK_RARE(bit(D, PK_DB_DAA))) {  // DAA (opcodes.py DAA_27), rare
             const u32 a = w1 >> 24;
             u32 corr = sel(F & 0x20u, 0x06u, 0u) | sel(F & 0x10u, 0x60u, 0u);
@@ -648,60 +637,78 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             nf = (F & 0x40u) | sel(res8 == 0u, 0x80u, 0u) | sel(corr & 0x60u, 0x10u, 0u);
         }
         // register writeback: val = res16 | F' << 16 | res8 << 24 through the per-op byte selectors
-        const u32 val = res16 | (nf << 16) | (res8 << 24);
+        // (res16: the adder, or HL +- 1 for (HL+)/(HL-); bytes 2-3 of either are not taken)
+        const u32 u16 = sel(bit(U, PK_US_R16HL), w1 + (u32)sfield(U, PK_US_HLINC, 2), r);
+        const u32 val = perm(nf | (res8 << 8), u16, 0x05040100u);
         s.w0 = perm(val, w0, S0);
         s.w1 = perm(val, w1, S1);
 
         // ---------------- control transfer, SP, IME/HALT ----------------
-        const u32 tsrc = (D >> PK_DB_TSRC) & 7u;
-        const u32 jrt = (pc + 2u + sx8) & 0xFFFFu;
-        const u32 tgt = sel(tsrc == PK_J_JR, jrt, (X | Y) & 0xFFFFu);  // JP/CALL/INT nn, JP HL, RET, RST: X | Y
-        const bool jump = tsrc != 0u && taken != 0u;
+        // JP/CALL/INT nn, JP HL, RET, RST: X | Y (one of them is 0); JR: pc + 2 + (Y = sext e)
+        const u32 tgt = (X + Y + (pcn & V)) & 0xFFFFu;
+        const bool jump = bit(U, PK_US_JUMP) != 0u && taken != 0u;
         s.pc = sel(jump, tgt, pcn);
         ev |= sel(jump, PK_EV_JUMP, 0u);
         u32 cycles = ((D >> PK_DB_CYC) & 7u) * 4u + sel(taken != 0u, ((D >> PK_DB_XCYC) & 3u) * 4u, 0u);
-        const u32 sp2 = (sp + ((u32)sfield(U, PK_UB_SPD, 3) & (0u - taken))) & 0xFFFFu;
-        s.sp = sel(bit(U, PK_UB_SPW), res16, sp2);
+        const u32 sp2 = (sp + ((u32)sfield(U, PK_US_SPD, 3) & (0u - taken))) & 0xFFFFu;
+        s.sp = sel(bit(U, PK_US_SPW), u16 & 0xFFFFu, sp2);
         {
             // IME / HALT / CRASH / QUEUED: (cpu & keep) | set from the microcode
-            s.cpu = (s.cpu & (0xFFFFFFF0u | ((K >> PK_KB_CPUAND) & 15u))) | (K >> PK_KB_CPUOR);
+            s.cpu = (s.cpu & (0xFFFFFFF0u | ((K >> 24) & 15u))) | (K >> 28);
         }
         // ---------------- fused secondary op (pk_ucode.h pk_u2_entry) ----------------
-        // The instruction after this one, if it is a JR (cc), LD r,r', INC/DEC BC/DE/HL or NOP, runs
-        // in this iteration on the registers and flags just written, as PyBoy's next cpu.tick would,
-        // when nothing could happen between the two: this instruction may fuse (PK_DB_FUSE: executed,
-        // no control transfer / IME / HALT / DAA), its cycles raise no LCD event or frame end (clock
-        // stays below the LCD target, or below the frame length with the LCD off) and no watchdog end,
-        // the timer is off (no TIMA overflow), it writes no IO/MBC register (slow write) and, when the
-        // code runs from RAM, nothing at all (the prefetched bytes stay valid).  Its bytes are among
-        // the 4 fetched ones (3 when the code is outside the ROM or within 3 bytes of a bank end) and
-        // none of them is an IO register (DIV and a folded STAT change with the clock).
+        // The instruction after this one, if it is a JR (cc), LD r,r', INC/DEC r, INC/DEC BC/DE/HL or
+        // NOP, runs in this iteration on the registers and flags just written, as PyBoy's next
+        // cpu.tick would, when nothing could happen between the two: this instruction may fuse (its
+        // PK_DB_NOFUSE bit clear: executed, no control transfer / IME / HALT / DAA), its cycles raise
+        // no LCD event (clock stays below the LCD target and the frame length: covers the LCD-off
+        // frame end too) and no watchdog frame end (slack), the timer is off (no TIMA overflow), and
+        // it writes no IO/MBC register (slow write).  Code in RAM also needs: no write at all (the
+        // fetched bytes stay valid), both instructions within the 3 bytes every fetch path provides
+        // (ROM code has 4), and none of them an IO register (DIV and a folded STAT change with the clock).
         const bool wr = bit(D, PK_DB_WR) != 0u && taken != 0u, wr2 = bit(D, PK_DB_WR2) != 0u;
         const bool wram = wr & fast01;
         {
             const u32 nxt = bytes >> (8u * (D & 3u));
-            const uint4 u2 = ucv2[nxt & 0xFFu];
-            const u32 M2 = u2.y;
-            const u32 len2 = (M2 >> PK_U2B_LEN) & 3u;
-            const bool nb4 = (pc < 0x8000u) & ((pc & 0x3FFFu) <= 0x3FFCu);
-            const u32 lim = sel(s.lcd0 & 0x80u, s.target, FRAME_CYCLES);
-            const bool fuse = (bit(D, PK_DB_FUSE) != 0u) & ((M2 & 3u) != 0u) & ((D & 3u) + len2 <= sel(nb4, 4u, 3u))
-                            & (s.clock + cycles < lim) & (budget + cycles + 1u <= 16u * FRAME_CYCLES) & !(s.tim0 & (4u << 24))
-                            & !(wr & (!wram | (pc >= 0x8000u))) & !(pc - 0xFEFEu < 0x82u);
-            // register ops: val2 = pair +- 1 (bytes 0-1) or the source register (byte 3), written back
-            // through the entry's selectors; JR: condition on the new F, target pc + 2 + e
-            const u32 v2 = perm(s.w1, s.w0, u2.x) + (u32)sfield(M2, PK_U2B_DELTA, 8);
-            const u32 w0f = perm(v2, s.w0, u2.z), w1f = perm(v2, s.w1, u2.w);
-            const u32 tk2 = ((((w1f >> 16) | 0x100u) >> ((M2 >> PK_U2B_CPOS) & 15u)) & 1u) ^ bit(M2, PK_U2B_CINV);
-            const bool jr2 = (M2 & 3u) == PK_U2_JR;
-            const u32 pc2 = (s.pc + len2 + sel(jr2 & (tk2 != 0u), (u32)(int)(int8_t)(u8)(nxt >> 8), 0u)) & 0xFFFFu;
+            const uint4 u2 = ucv2[(nxt & 0xFFu) | (D & (1u << PK_DB_NOFUSE))];
+            const u32 len2 = u2.y & 3u;
+            // both instructions within the fetched bytes: 4 for ROM code, 3 for code in RAM
+            const bool lenok = (D & 3u) + len2 + sel(pc >= 0x8000u, 1u, 0u) <= 4u;
+            const bool ramok = (pc < 0x8000u) | (!wr & !(pc - 0xFEFEu < 0x82u));
+            const u32 lim = sel(s.lcd0 & 0x80u, s.target, FRAME_CYCLES);   // next LCD event / LCD-off frame end
+            const bool fuse = (len2 != 0u) & ((int)cycles < slack) & (s.clock + cycles < lim)
+                            & !(s.tim0 & (4u << 24)) & !(wr & !wram) & ramok & lenok;
+            const u32 M2 = sel(fuse, u2.y, PK_U2_NONE_Y);
+            // operand (pair, or register in byte 0) + delta; INC/DEC r flags: Z N H replace F's bits
+            // under the entry's mask, C kept; val2 = r16 | F' << 16 | r8 << 24 through the selectors
+            const u32 x = perm(s.w1, s.w0, u2.x);
+            const int dl = sfield(M2, PK_U2B_DELTA, 8);
+            const u32 r = x + (u32)dl;
+            const u32 nz = sel((r & 0xFFu) == 0u, 0x80u, 0u) | ((u32)dl & 0x40u);
+            const u32 zh = nz | (((x ^ r) << 1) & ~0xC0u);   // Z N from nz, H = carry into bit 4
+            const u32 F1 = (s.w1 >> 16) & 0xFFu;
+            const u32 fm = M2 >> PK_U2B_FM;
+            const u32 Fn = (zh & fm) | (F1 & ~fm);
+            const u32 val2 = perm(Fn, r, 0x00040100u);
+            const u32 w0f = perm(val2, s.w0, sel(fuse, u2.z, PK_S0_ID));
+            const u32 w1f = perm(val2, s.w1, sel(fuse, u2.w, PK_S1_ID));
+            // JR: taken when (F & mask) == cv (mask at F's byte of the x word, cv at the same byte of
+            // the misc word; never for the other entries and when not fused)
+            const bool tk2 = (((s.w1 & u2.x) ^ M2) & 0x00FF0000u) == 0u;
+            const u32 pc2 = (s.pc + (M2 & 3u) + sel(tk2, (u32)sfield(nxt, 8, 8), 0u)) & 0xFFFFu;
             if (fuse) PK_TRACE(env, s.pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, nxt & 0xFFu);
-            s.w0 = sel(fuse, w0f, s.w0);
-            s.w1 = sel(fuse, w1f, s.w1);
-            s.pc = sel(fuse, pc2, s.pc);
-            cycles += sel(fuse, ((M2 >> PK_U2B_CYC) & 15u) * 4u + sel(jr2 & (tk2 != 0u), 4u, 0u), 0u);
-            budget += sel(fuse, 1u, 0u);
-            icount += sel(fuse, 1u, 0u);
+            ev |= sel(fuse, PK_EV_FUSE, 0u);
+#ifdef PK_DBG_FUSE
+            ev |= sel(len2 != 0u, 1u << 23, 0u) | sel((int)cycles < slack, 1u << 24, 0u) | sel(s.clock + cycles < lim, 1u << 25, 0u)
+                | sel(!(s.tim0 & (4u << 24)), 1u << 26, 0u) | sel(!(wr & !wram) & ramok, 1u << 27, 0u);
+#endif
+            s.w0 = w0f;
+            s.w1 = w1f;
+            s.pc = pc2;
+            const u32 one = bit(M2, PK_U2B_ONE);
+            cycles += ((M2 >> PK_U2B_CYC) & 15u) * 4u + sel(tk2, 4u, 0u);
+            slack -= (int)one;
+            icount += one;
         }
 
         // priority 2 from here (the writes and the next instruction's address): above a wave in its
@@ -720,10 +727,9 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         }
 
         // ---------------- memory writes (wv0 at addr0, wv1 at addr1) ----------------
-        const u32 pushv = sel(bit(U, PK_UB_WPC), pcn, sel(bit(U, PK_UB_WSP), sp, Y & 0xFFFFu));
-        const u32 wv = sel(bit(U, PK_UB_W16), pushv, res8);
-        const bool hifirst = bit(D, PK_DB_ADIR + 1) != 0u;  // adir = -1: push writes the high byte first
-        const u32 wv0 = sel(hifirst, wv >> 8, wv) & 0xFFu, wv1 = sel(hifirst, wv, wv >> 8) & 0xFFu;
+        // 16-bit writes: low byte at addr0, high byte at addr1 (pushes: SP-2, SP-1)
+        const u32 wv = sel(bit(U, PK_US_W16), sel(bit(U, PK_US_WPC), pcn, X), res8);
+        const u32 wv0 = wv & 0xFFu, wv1 = (wv >> 8) & 0xFFu;
         if (wram) {
             // VRAM / OAM change while rendered lines are pending: rasterise them first (rare)
             // (lines are pending only in the rendered frame: test that first, alone)
@@ -747,7 +753,8 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         PK_STAMP_AT(2);
         if (PK_RARE(wr & !wram)) {  // rare: IO registers / MBC / SRAM / OAM DMA / IE
             St t = s;
-            pk_write_slow(&A, c.g, c.lane, c.loc, env, c.gid, &t, addr0, wv0, addr1, wv1, wr2 ? 1u : 0u);
+            pk_write_slow(&A, c.g, c.lane, c.loc, env, c.gid, &t, addr0, wv0, addr1, wv1, wr2 ? 1u : 0u,
+                          bit(U, PK_US_HIFIRST));
             s = t;
             ev |= PK_EV_WR_SLOW;
             PK_STAMP_AT(3);
@@ -780,9 +787,10 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             const u32 op = pbytes & 0xFFu;
             PK_STAMP_AT(4);
             const u32 di = sel(op == 0xCBu, 256u + ((pbytes >> 8) & 0xFFu), op);
-            p0 = ucv[di * 3u];
-            p1 = ucv[di * 3u + 1u];
-            p2 = ucv[di * 3u + 2u];
+            p0 = ucv[di * 4u];
+            p1 = ucv[di * 4u + 1u];
+            p2 = ucv[di * 4u + 2u];
+            p3 = ucv[di * 4u + 3u];
             pf = sel(fl | fh | fg, 1u, 0u);
         }
 
@@ -808,7 +816,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             const u32 vbl = sel(nm == 2u, s.target + 456u * lines, s.target - sel(nm == 3u, 80u, 250u) + 456u * (lines + 1u));
             const u32 nev = sel(nm == 3u, 2u, sel(nm == 0u, 1u, 0u)) + 3u * lines + 1u;  // iterations up to VBlank
             const u32 tnew = vbl - 206u;                                                  // line 143 mode-0 event
-            if (cand && budget + (vbl - s.clock) + nev <= 16u * FRAME_CYCLES) {
+            if (cand && (int)((vbl - s.clock) + nev) <= slack) {
                 if (s.render) {
                     // rendered frame: the skipped mode-0 events would latch every remaining line with
                     // the (unchanging, the CPU is halted) scroll/window/palette registers — latch
@@ -831,7 +839,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
                 }
                 const u32 skipped = tnew - s.clock;
                 s.divacc = (s.divacc + skipped) & 0xFFFFu;
-                budget += skipped + (nev - 1u);
+                slack -= (int)(skipped + (nev - 1u));
                 s.clock = tnew;
                 s.target = vbl;
                 const u32 st2 = (stat & 0xF8u) | sel((s.lcd0 >> 24) == 143u, 4u, 0u);
@@ -917,14 +925,14 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         }
         s.cpu |= irq << 16;
         PK_STAMP_AT(7);
-        budget += cycles + 1u;
-        ev |= sel(s.frame_done != 0u || budget > 16u * FRAME_CYCLES, PK_EV_FRAME, 0u);
+        slack -= (int)(cycles + 1u);
+        ev |= sel(s.frame_done != 0u || slack < 0, PK_EV_FRAME, 0u);
         PK_ITER(env, ev);
-        PK_ITER_OP(env, sel(exec, sel((bytes & 0xFFu) == 0xCBu, 256u + b1, bytes & 0xFFu),
+        PK_ITER_OP(env, sel(exec, sel((bytes & 0xFFu) == 0xCBu, 256u + ((bytes >> 8) & 0xFFu), bytes & 0xFFu),
                             sel(dispatch, PK_UC_INT, sel(doint, PK_UC_NOP0, PK_UC_IDLE))));
-        if (PK_RARE((s.frame_done != 0u) | (budget > 16u * FRAME_CYCLES))) {  // frame end or watchdog
+        if (PK_RARE((s.frame_done != 0u) | (slack < 0))) {  // frame end or watchdog
             s.frame_done = 0;
-            budget = 0;
+            slack = (int)(16u * FRAME_CYCLES);
             frame += 1u;
             if (frame == A.release_frame && btn != 0xFFu) key_event(s, btn, false);
             s.render = (A.render_last && frame + 1u == A.frames) ? 1u : 0u;

@@ -18,17 +18,38 @@
 #pragma once
 #include <stdint.h>
 
-// ---- entry layout: 12 dwords (three ds_read_b128) ----
+// ---- entry layout: 16 dwords (four ds_read_b128) ----
 enum { PK_UE_D = 0, PK_UE_U, PK_UE_K, PK_UE_V, PK_UE_XR, PK_UE_XE, PK_UE_YR, PK_UE_YE, PK_UE_AR, PK_UE_AE,
-       PK_UE_S0, PK_UE_S1, PK_UE_WORDS };
+       PK_UE_S0, PK_UE_S1, PK_UE_YC, PK_UE_YX, PK_UE_CW, PK_UE_CI, PK_UE_WORDS };
+// stored words (what the kernel reads; the builder below works in the PK_UB_/PK_KB_ form):
+//   U  datapath control bits PK_US_*          K  FC | FK << 8 | FM << 16 | CPUAND << 24 | CPUOR << 28
+//   V  0xFFFF for JR (target = pc + len + Y), else 0
+//   YC Y constant (INC/DEC, CPL, BIT/RES/SET masks, RST vector)   YX 0x1FFFF when the adder subtracts
+//   CW/CI carry-in (adder) / shifted-in bit (right-shift unit) = bit CW of (X | F << 16) ^ CI:
+//         bit 20 = F.C, bit 7/bit 0 = X's top/bottom bit, bit 16 = constant 0 (with CI: constant 1)
+#define PK_US_HSH8 0      // H/C from carry bits 12/16 (ADD HL,rr), else 4/8
+#define PK_US_RIGHT 1     // result8 and C from the right-shift unit
+#define PK_US_SWAP 2      // right-shift unit: nibble swap
+#define PK_US_LOGIC 3     // result8 from the logic unit (loads: X = 0xFF AND Y), else adder / right unit
+#define PK_US_JUMP 4      // control transfer to X + Y (+ pc + len for JR) when the condition holds
+#define PK_US_WPC 5       // 16-bit write value = return PC (else X)
+#define PK_US_W16 6       // write value 16-bit (else result8)
+#define PK_US_HIFIRST 7   // a 16-bit push: the slow bus path writes the high address first (PyBoy order)
+#define PK_US_FPOP 8      // F = m0 & 0xF0 (POP AF)
+#define PK_US_R16HL 9     // res16 = HL +- 1 (else adder)
+#define PK_US_SPW 10      // SP = res16
+#define PK_US_LAND 12     // logic result includes X & Y (AND, OR)
+#define PK_US_LXOR 13     // logic result includes X ^ Y (XOR, OR)
+#define PK_US_HLINC 22    // 2 bits signed HL increment for (HL+)/(HL-)
+#define PK_US_SPD 26      // 3 bits signed SP delta (PUSH/POP family), applied when the condition holds
 #define PK_UC_ENTRIES 515u
 #define PK_UC_INT 512u    // pseudo-op: interrupt dispatch (push PC, jump to the vector)
 #define PK_UC_IDLE 513u   // pseudo-op: halted / crashed CPU, 4 cycles
 #define PK_UC_NOP0 514u   // pseudo-op: interrupt pending with IME off (queued), 0 cycles
-// secondary-op table (fused pairs, see pk_u2_entry): 256 entries x 4 dwords after the main table
+// secondary-op table (fused pairs, see pk_u2_entry): 512 entries x 4 dwords after the main table
 #define PK_U2_WORDS 4u
 #define PK_UC_U2 (PK_UC_ENTRIES * PK_UE_WORDS)
-#define PK_UC_WORDS (PK_UC_U2 + 256u * PK_U2_WORDS)
+#define PK_UC_WORDS (PK_UC_U2 + 512u * PK_U2_WORDS)
 
 // D word: memory, timing, control
 #define PK_DB_LEN 0       // 2 bits  instruction length
@@ -37,7 +58,7 @@ enum { PK_UE_D = 0, PK_UE_U, PK_UE_K, PK_UE_V, PK_UE_XR, PK_UE_XE, PK_UE_YR, PK_
 #define PK_DB_WR 4        // write wv0 at addr0
 #define PK_DB_WR2 5       // write wv1 at addr1
 #define PK_DB_ASP 6       // (builder only) address source SP        -> AE selector
-#define PK_DB_FUSE 6      // (stored word) a secondary op may follow in the same iteration (pk_u2_entry)
+#define PK_DB_NOFUSE 8    // (stored word) no secondary op may follow in the same iteration (pk_u2_entry)
 #define PK_DB_AIMM 7      // (builder only) address source immediate -> AE selector
 #define PK_DB_AHN 8       // (builder only) immediate address 0xFF00|n
 #define PK_DB_AOFF 9      // 2 bits signed: addr0 = src + aoff
@@ -422,26 +443,34 @@ static inline PkUop pk_uop_cb(int op) {
 }
 
 // the whole table: [0,256) base, [256,512) CB-prefixed, then the three pseudo-ops
+static inline uint32_t pk_has_res8(uint32_t s) {   // a writeback selector taking val byte 3 (result8)
+    for (int b = 0; b < 4; b++)
+        if (((s >> (8 * b)) & 0xFFu) == 0x07u) return 1u;
+    return 0u;
+}
 static inline void pk_store_uop(uint32_t* e, PkUop o, bool real) {
+    for (int w = 0; w < (int)PK_UE_WORDS; w++) e[w] = 0;
     // CPU state update as (cpu & keep) | set: IME from DI/EI/RETI/INT, HALT, CRASH; an executed
     // instruction clears QUEUED (pyboy cpu.tick), the pseudo-ops keep it
+    uint32_t cpu_keep = 0xFu, cpu_set = 0u;
     {
         const uint32_t ime = (o.d >> PK_DB_IME) & 3u;
-        uint32_t keep = 0xFu, set = 0u;
-        if (real) keep &= ~4u;
-        if (ime == 1u) keep &= ~1u;
-        if (ime == 2u) set |= 1u;
-        if (o.d & pk_fld(1, PK_DB_HALT)) set |= 2u;
-        if (o.d & pk_fld(1, PK_DB_CRASH)) set |= 2u | 8u;
-        o.k |= pk_fld(keep, PK_KB_CPUAND) | pk_fld(set, PK_KB_CPUOR);
+        if (real) cpu_keep &= ~4u;
+        if (ime == 1u) cpu_keep &= ~1u;
+        if (ime == 2u) cpu_set |= 1u;
+        if (o.d & pk_fld(1, PK_DB_HALT)) cpu_set |= 2u;
+        if (o.d & pk_fld(1, PK_DB_CRASH)) cpu_set |= 2u | 8u;
     }
+    uint32_t us = 0, jrm = 0;
+    uint32_t yc = o.k & 0xFFu, yx = 0, cw = 0, ci = 0;
+    const uint32_t r8 = (o.u >> PK_UB_R8) & 3u, lop = (o.u >> PK_UB_LOP) & 3u, fcs = (o.u >> PK_UB_FC) & 3u;
+    const bool sub = (o.u & pk_fld(1, PK_UB_SUB)) != 0u, usec = (o.u & pk_fld(1, PK_UB_USEC)) != 0u;
+    const bool w16 = (o.u & pk_fld(1, PK_UB_W16)) != 0u, wr = (o.d & pk_fld(1, PK_DB_WR)) != 0u;
     // jump targets through the operand pools: JP/CALL/INT nn -> Y = nn, JP HL -> X = HL,
-    // RET -> Y = m16, RST -> Y = yconst (the vector); the datapath result of these ops is unused
+    // RET -> Y = m16, RST -> Y = yconst (the vector), JR -> pc + len + (Y = sign-extended e)
     const uint32_t ts = (o.d >> PK_DB_TSRC) & 7u;
-    uint32_t js = PK_J_NONE;
-    if (ts == PK_T_JR) js = PK_J_JR;
-    else if (ts != PK_T_NONE) {
-        js = PK_J_XY;
+    if (ts != PK_T_NONE) {
+        us |= pk_fld(1, PK_US_JUMP);
         o.u &= ~(pk_fld(1, PK_UB_XSP) | pk_fld(1, PK_UB_XMEM) | pk_fld(1, PK_UB_YIMM) | pk_fld(1, PK_UB_IMM8) |
                  pk_fld(1, PK_UB_SEXT) | pk_fld(1, PK_UB_YMEM));
         o.px = PK_PZERO;
@@ -449,30 +478,91 @@ static inline void pk_store_uop(uint32_t* e, PkUop o, bool real) {
         if (ts == PK_T_IMM) o.u |= pk_fld(1, PK_UB_YIMM);
         if (ts == PK_T_HL) o.px = pk_sel16(2);
         if (ts == PK_T_M16) o.u |= pk_fld(1, PK_UB_YMEM);
+        if (ts == PK_T_JR) { o.u |= pk_fld(1, PK_UB_YIMM) | pk_fld(1, PK_UB_SEXT); jrm = 0xFFFFu; }
+        if (ts != PK_T_RST) yc = 0;
     }
-    o.d = (o.d & ~(7u << PK_DB_TSRC)) | pk_fld(js, PK_DB_TSRC);
-    // operand sources -> ext-pool selectors (the register-pool selector is zeroed when unused)
+    o.d &= ~(7u << PK_DB_TSRC);
+    // 16-bit writes: the value is X (PUSH: the pair, LD (nn),SP: SP) or the return PC; pushes go to
+    // SP-2 (low byte) and SP-1 (high byte), the slow path writes the high byte first as PyBoy does
+    bool push = false;
+    if (w16) {
+        us |= pk_fld(1, PK_US_W16);
+        if (o.u & pk_fld(1, PK_UB_WPC)) us |= pk_fld(1, PK_US_WPC);
+        else if (o.u & pk_fld(1, PK_UB_WSP)) o.u |= pk_fld(1, PK_UB_XSP);
+        else { o.px = o.py; o.py = PK_PZERO; }   // PUSH rr: X = the pair
+        if (((o.d >> PK_DB_ADIR) & 3u) == 3u) {   // adir -1: a push
+            push = true;
+            o.d = (o.d & ~(15u << PK_DB_AOFF)) | pk_sfld(-2, PK_DB_AOFF, 2) | pk_sfld(1, PK_DB_ADIR, 2);
+            us |= pk_fld(1, PK_US_HIFIRST);
+        }
+    }
+    (void)push;
+    // result8: loads (builder R8 = 0, Y) go through the logic unit as 0xFF AND Y when result8 is used
+    if (r8 == 0u && (pk_has_res8(o.s0) || pk_has_res8(o.s1) || (wr && !w16))) {
+        o.px = 0x0C0C0C0Du;
+        o.u &= ~(pk_fld(1, PK_UB_XSP) | pk_fld(1, PK_UB_XMEM));
+        us |= pk_fld(1, PK_US_LOGIC) | pk_fld(1, PK_US_LAND);
+    }
+    if (r8 == 2u) {
+        us |= pk_fld(1, PK_US_LOGIC) | pk_fld(lop != 1u ? 1u : 0u, PK_US_LAND) | pk_fld(lop != 0u ? 1u : 0u, PK_US_LXOR);
+    }
+    if (sub) yx = 0x1FFFFu;
+    // carry-in of the adder: SUB ^ (USEC & F.C)
+    if (usec) { cw = 1u << 20; ci = sub ? (1u << 20) : 0u; }
+    else if (sub) { cw = 1u << 16; ci = 1u << 16; }
+    const uint32_t rbin = (o.u >> PK_UB_RBIN) & 3u;
+    if (r8 == 3u) {
+        const bool rdir = (o.u & pk_fld(1, PK_UB_RDIR)) != 0u;
+        if (o.u & pk_fld(1, PK_UB_SWAP)) {
+            us |= pk_fld(1, PK_US_RIGHT) | pk_fld(1, PK_US_SWAP);
+        } else if (rdir) {   // RRC RRCA RR RRA SRA SRL: shifted-in bit 0 / F.C / bit 0 (rotated out) / bit 7
+            static const uint32_t rb[4] = {0u, 1u << 20, 1u << 0, 1u << 7};
+            us |= pk_fld(1, PK_US_RIGHT);
+            cw = rb[rbin];
+        } else {             // RLC RLCA RL RLA SLA: the adder, X + X + (0 / F.C / bit 7)
+            static const uint32_t lb[4] = {0u, 1u << 20, 1u << 7, 0u};
+            o.py = o.px;
+            if (o.u & pk_fld(1, PK_UB_XMEM)) o.u |= pk_fld(1, PK_UB_YMEM);
+            cw = lb[rbin];
+            ci = 0;
+        }
+    }
+    if (fcs == 3u) {   // CCF: C = !F.C through the adder, 0xFF + 0 + !F.C
+        o.px = 0x0C0C0C0Du;
+        cw = 1u << 20;
+        ci = 1u << 20;
+    }
+    if (o.u & pk_fld(1, PK_UB_HC16)) us |= pk_fld(1, PK_US_HSH8);
+    if (o.u & pk_fld(1, PK_UB_FPOP)) us |= pk_fld(1, PK_US_FPOP);
+    if (o.u & pk_fld(1, PK_UB_R16HL)) us |= pk_fld(1, PK_US_R16HL);
+    if (o.u & pk_fld(1, PK_UB_SPW)) us |= pk_fld(1, PK_US_SPW);
+    us |= o.u & ((3u << PK_UB_HLINC) | (7u << PK_UB_SPD));   // same positions as PK_US_HLINC / PK_US_SPD
+    // flags: F' = (F & FK) | ((Z | H | C | FC) & FM)
+    const uint32_t fkeep = (o.k >> PK_KB_FKEEP) & 0xFFu, fconst = (o.k >> PK_KB_FCONST) & 0xFFu;
+    uint32_t fm = fconst;
+    if (o.u & pk_fld(1, PK_UB_FZ)) fm |= 0x80u;
+    if (o.u & pk_fld(1, PK_UB_FH)) fm |= 0x20u;
+    if (fcs != 0u) fm |= 0x10u;
+    // operand sources -> ext-pool selectors (the register-pool selector is zeroed when unused);
+    // a memory operand is m0 for one-byte reads, m0|m1 for two
+    const bool rd2 = (o.d & pk_fld(1, PK_DB_RD2)) != 0u;
     uint32_t xe = PK_PZERO, ye = PK_PZERO, ae = PK_PZERO;
     if (o.u & pk_fld(1, PK_UB_XSP)) xe = PK_E_SP;
     else if (o.u & pk_fld(1, PK_UB_XMEM)) xe = PK_E_M0;
     if (o.u & pk_fld(1, PK_UB_YIMM)) ye = (o.u & pk_fld(1, PK_UB_SEXT)) ? PK_E_SEXTN : (o.u & pk_fld(1, PK_UB_IMM8)) ? PK_E_N : PK_E_NN;
-    else if (o.u & pk_fld(1, PK_UB_YMEM)) ye = PK_E_M16;
+    else if (o.u & pk_fld(1, PK_UB_YMEM)) ye = rd2 ? PK_E_M16 : PK_E_M0;
     else if (o.d & pk_fld(1, PK_DB_YSP)) ye = PK_E_SP;
     if (o.d & pk_fld(1, PK_DB_ASP)) ae = PK_E_SP;
     else if (o.d & pk_fld(1, PK_DB_AIMM)) ae = (o.d & pk_fld(1, PK_DB_AHN)) ? PK_E_HN : PK_E_NN;
     e[PK_UE_D] = o.d & ~(pk_fld(1, PK_DB_ASP) | pk_fld(1, PK_DB_AIMM) | pk_fld(1, PK_DB_AHN) | pk_fld(1, PK_DB_YSP));
     // a secondary op may be fused after this one: executed instructions without control transfer,
     // IME/HALT/STOP changes or the rare DAA path (pk_u2_entry states the remaining conditions)
-    if (real && ts == PK_T_NONE && !(o.d & (pk_fld(3, PK_DB_IME) | pk_fld(1, PK_DB_HALT) | pk_fld(1, PK_DB_CRASH) |
-                                            pk_fld(1, PK_DB_DAA))) && (o.d & 3u) != 0u)
-        e[PK_UE_D] |= pk_fld(1, PK_DB_FUSE);
-    e[PK_UE_U] = o.u & ~63u;
-    e[PK_UE_K] = o.k;
-    // V word: datapath selectors derived from U in the form the kernel consumes in one op
-    {
-        const uint32_t r8 = (o.u >> PK_UB_R8) & 3u, lop = (o.u >> PK_UB_LOP) & 3u;
-        e[PK_UE_V] = pk_fld(8u * r8, PK_VB_R8SH) | pk_fld(lop != 1u ? 1u : 0u, PK_VB_LAND) | pk_fld(lop != 0u ? 1u : 0u, PK_VB_LXOR);
-    }
+    if (!(real && ts == PK_T_NONE && !(o.d & (pk_fld(3, PK_DB_IME) | pk_fld(1, PK_DB_HALT) | pk_fld(1, PK_DB_CRASH) |
+                                              pk_fld(1, PK_DB_DAA))) && (o.d & 3u) != 0u))
+        e[PK_UE_D] |= pk_fld(1, PK_DB_NOFUSE);
+    e[PK_UE_U] = us;
+    e[PK_UE_K] = fconst | (fkeep << 8) | (fm << 16) | (cpu_keep << 24) | (cpu_set << 28);
+    e[PK_UE_V] = jrm;
     e[PK_UE_XR] = xe != PK_PZERO ? PK_PZERO : o.px;
     e[PK_UE_XE] = xe;
     e[PK_UE_YR] = ye != PK_PZERO ? PK_PZERO : o.py;
@@ -481,51 +571,63 @@ static inline void pk_store_uop(uint32_t* e, PkUop o, bool real) {
     e[PK_UE_AE] = ae;
     e[PK_UE_S0] = o.s0;
     e[PK_UE_S1] = o.s1;
+    e[PK_UE_YC] = yc;
+    e[PK_UE_YX] = yx;
+    e[PK_UE_CW] = cw;
+    e[PK_UE_CI] = ci;
 }
 
 // ---- secondary ops: fused into the iteration of the instruction before them ----
 // The SIMT loop pays for one iteration per emulated instruction whatever the instruction, so the
 // cheap register-only successors of an instruction run in the same iteration: a JR (cc), LD r,r',
-// INC/DEC BC/DE/HL or NOP right after a fusable instruction (PK_DB_FUSE) executes on the registers
+// INC/DEC r, INC/DEC BC/DE/HL or NOP right after a fusable instruction executes on the registers
 // and flags that instruction left, exactly as the next cpu.tick would, when nothing can happen in
-// between — the instruction raised no LCD event, timer overflow or frame end, wrote no IO/IE/IF/MBC
-// register and no RAM code (pk_step.hip states the test).  Entry: x = val2 selector over w1:w0,
-// y = misc (class, length, cycles, condition, delta), z/w = writeback selectors (as S0/S1).
-enum { PK_U2_NONE = 0, PK_U2_REG = 1, PK_U2_JR = 2 };
-#define PK_U2B_LEN 2      // 2 bits length
+// between (pk_step.hip states the test).  The table has 512 entries: index = opcode | the primary's
+// PK_DB_NOFUSE bit (entries 256-511 are empty).  Entry: x = operand selector over w1:w0 (the pair,
+// or the source/target register, into byte 0), y = misc (length, cycles, JR condition, delta, flag
+// mask), z/w = writeback selectors of val2 = r16 | F' << 16 | r8 << 24 (as S0/S1).
+#define PK_U2B_LEN 0      // 2 bits length (0: no secondary op)
+#define PK_U2B_ONE 2      // 1: counts as an executed instruction
 #define PK_U2B_CYC 4      // 4 bits cycles/4 (JR: not taken)
-#define PK_U2B_CPOS 8     // 4 bits: JR condition = bit cpos of (F | 0x100) ...
-#define PK_U2B_CINV 12    //         ^ cinv
-#define PK_U2B_DELTA 16   // 8 bits signed: val2 = pair + delta (INC/DEC rr)
+#define PK_U2B_DELTA 8    // 8 bits signed: r = operand + delta (INC/DEC)
+#define PK_U2B_CV 16      // 8 bits: JR taken when (F & mask) == cv, the mask in byte 2 of the x word;
+                          //         1 for every other entry (F's low nibble is 0: never)
+#define PK_U2B_FM 24      // 8 bits: F bits replaced by Z N H (INC/DEC r: 0xE0), the rest kept
+#define PK_U2_NONE_Y (1u << PK_U2B_CV)
 static inline void pk_u2_entry(uint32_t* e, int op) {
-    uint32_t cls = PK_U2_NONE, len = 1, cyc = 4, cpos = 8, cinv = 0;
+    uint32_t len = 0, cyc = 0, cv = 1, fm = 0;
     int delta = 0;
-    PkUop o = pk_uop_base(1, 4);
-    o.s1 = PK_S0_ID;   // identity writeback of both words (val2 has no flags byte), zero val2 source
-    uint32_t sel2 = PK_PZERO;
-    if (op == 0x00) {
-        cls = PK_U2_REG;
-    } else if (op >= 0x40 && op < 0x80 && op != 0x76 && (op & 7) != 6 && ((op >> 3) & 7) != 6) {  // LD r, r'
-        cls = PK_U2_REG;
-        sel2 = 0x000C0C0Cu | (pk_r8_byte(op & 7) << 24);   // r' -> val2 byte 3 (the result8 slot)
-        pk_wb_r8(o, (op >> 3) & 7);
-    } else if ((op & 0xC7) == 0x03 && ((op >> 4) & 3) != 3) {  // INC rr / DEC rr (BC DE HL)
-        const int p = (op >> 4) & 3;
-        cls = PK_U2_REG;
-        cyc = 8;
-        sel2 = pk_sel16(p);
-        delta = (op & 8) ? -1 : 1;
-        pk_wb_r16(o, p);
-    } else if (op == 0x18 || op == 0x20 || op == 0x28 || op == 0x30 || op == 0x38) {  // JR (cc,) e
-        static const uint32_t pos[4] = {7, 7, 4, 4}, inv[4] = {1, 0, 1, 0};
-        cls = PK_U2_JR;
-        len = 2;
-        cyc = 8;   // + 4 when taken
-        if (op != 0x18) { cpos = pos[(op >> 3) & 3]; cinv = inv[(op >> 3) & 3]; }
+    PkUop o = pk_uop_base(1, 4);   // identity writeback selectors (F from val2 = F' = F unless fm)
+    uint32_t sel = PK_PZERO;
+    if (op < 256) {
+        if (op == 0x00) {
+            len = 1; cyc = 4;
+        } else if (op >= 0x40 && op < 0x80 && op != 0x76 && (op & 7) != 6 && ((op >> 3) & 7) != 6) {  // LD r, r'
+            len = 1; cyc = 4;
+            sel = pk_sel8(op & 7);
+            pk_wb_r8(o, (op >> 3) & 7);
+        } else if ((op & 0xC6) == 0x04 && ((op >> 3) & 7) != 6) {  // INC r / DEC r: Z N H, C kept
+            const int r = (op >> 3) & 7;
+            len = 1; cyc = 4; fm = 0xE0;
+            sel = pk_sel8(r);
+            delta = (op & 1) ? -1 : 1;
+            pk_wb_r8(o, r);
+        } else if ((op & 0xC7) == 0x03 && ((op >> 4) & 3) != 3) {  // INC rr / DEC rr (BC DE HL), no flags
+            const int p = (op >> 4) & 3;
+            len = 1; cyc = 8;
+            sel = pk_sel16(p);
+            delta = (op & 8) ? -1 : 1;
+            pk_wb_r16(o, p);
+        } else if (op == 0x18 || op == 0x20 || op == 0x28 || op == 0x30 || op == 0x38) {  // JR (cc,) e
+            static const uint32_t msk[4] = {0x80, 0x80, 0x10, 0x10}, val[4] = {0, 0x80, 0, 0x10};  // NZ Z NC C
+            len = 2; cyc = 8;   // + 4 when taken
+            sel = op == 0x18 ? 0u : msk[(op >> 3) & 3] << 16;   // JR e: mask 0 -> always taken
+            cv = op == 0x18 ? 0u : val[(op >> 3) & 3];
+        }
     }
-    e[0] = sel2;
-    e[1] = cls | (len << PK_U2B_LEN) | ((cyc / 4u) << PK_U2B_CYC) | (cpos << PK_U2B_CPOS) | (cinv << PK_U2B_CINV)
-         | (((uint32_t)delta & 0xFFu) << PK_U2B_DELTA);
+    e[0] = sel;
+    e[1] = (len << PK_U2B_LEN) | ((len ? 1u : 0u) << PK_U2B_ONE) | ((cyc / 4u) << PK_U2B_CYC)
+         | (((uint32_t)delta & 0xFFu) << PK_U2B_DELTA) | (cv << PK_U2B_CV) | (fm << PK_U2B_FM);
     e[2] = o.s0;
     e[3] = o.s1;
 }
@@ -544,5 +646,5 @@ static inline void pk_build_ucode(uint32_t* t /* PK_UC_WORDS */) {
     PkUop idle = pk_uop_base(0, 4), nop0 = pk_uop_base(0, 0);
     const PkUop ps[3] = {it, idle, nop0};
     for (int j = 0; j < 3; j++) pk_store_uop(t + (size_t)(512 + j) * PK_UE_WORDS, ps[j], false);
-    for (int op = 0; op < 256; op++) pk_u2_entry(t + PK_UC_U2 + (size_t)op * PK_U2_WORDS, op);
+    for (int op = 0; op < 512; op++) pk_u2_entry(t + PK_UC_U2 + (size_t)op * PK_U2_WORDS, op);
 }

@@ -17,7 +17,7 @@ from pokegym_amd.testrom.game import game_rom  # noqa: E402
 
 NAMES = ["EXEC", "F_LDS", "F_ROM16", "F_BUS", "INT", "IDLE", "RD", "RD_ROMLDS", "RD_ROMG", "RD_RAM", "RD_IO",
          "RD2", "WR", "WR_SLOW", "WR2", "LCD", "TIMER", "FRAME", "FLUSH", "HRAM", "JUMP", "CB",
-         "FAM_LD8", "FAM_ALU", "FAM_BITROT", "FAM_16", "FAM_CTRL", "FAM_MISC", "RD_WRAM", "WR_WRAM", "WR_VRAM", "WR_HI"]
+         "FUSE", "FAM_ALU", "FAM_BITROT", "FAM_16", "FAM_CTRL", "FAM_MISC", "RD_WRAM", "WR_WRAM", "WR_VRAM", "WR_HI"]
 
 
 def main():
