@@ -21,7 +21,7 @@ HEAT_SHAPE = (444, 436)
 OBS_SHAPE = (72, 80, 4)
 # PK_ERR_* -> the exception the reference raises at that point (include/pokegym_amd.h)
 ERR_EXCEPTIONS = {1: KeyError, 2: AttributeError, 3: IndexError, 4: UnboundLocalError, 5: IndexError,
-                  6: IndexError, 7: MemoryError}
+                  6: IndexError, 7: MemoryError, 8: ValueError}
 STATE_V9_BYTES = 142610
 ROWS, COLS = 144, 160
 

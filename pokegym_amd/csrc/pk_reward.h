@@ -62,6 +62,7 @@ enum { RSD_LAST_REWARD = 0, RSD_TOTAL_HEALING, RSD_LAST_HP, RSD_COORD /* np.sum(
 #define PKE_HEATMAP_INDEX 5u
 #define PKE_BUS_INDEX 6u
 #define PKE_CAPACITY 7u       // device table full (no reference equivalent)
+#define PKE_EMPTY_PARTY 8u    // ValueError: max(party_levels) of an empty party in the info dict (:1672)
 
 // info telemetry record (environment.py:1621-1704; field order = pokegym_amd/info.py FIELDS)
 #define PK_INFO_NSTATS 58u

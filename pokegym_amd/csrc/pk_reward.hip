@@ -551,11 +551,13 @@ __global__ void __launch_bounds__(256) pk_reward_kernel(PkRewardArgs A) {
 
     // info telemetry (:1621-1704): built on done or every 10000th step; rare, so its extra peeks
     // stay off the common path.  Every numeric scalar of info["stats"] / info["reward"].
-    if (A.info && !M.err && (done || time % 10000u == 0u)) {
+    if (!M.err && (done || time % 10000u == 0u)) {
         u32 lv[6], hi = 0;
         for (u32 k = 0; k < 6u; k++) { lv[k] = rd(M, k_party_level[k]); hi = max(hi, lv[k]); }
-        {   // highest_pokemon_level = max(nonzero levels); the reference raises ValueError (max([]),
-            // :1672) for an empty party — telemetry does not kill the env here, the record holds 0
+        // highest_pokemon_level = max(nonzero levels): for an empty party the reference raises
+        // ValueError (max([]), :1672) after every state update of the step — PK_ERR_EMPTY_PARTY
+        if (hi == 0u) M.err = PKE_EMPTY_PARTY;
+        if (A.info && !M.err) {
             const u32 nb = badges_reward / 10u;
             const u32 d7b1 = rd(M, 0xD7B1);
             auto bcd = [](u32 v) { return 10u * ((v >> 4) & 0xFu) + (v & 0xFu); };

@@ -5,8 +5,9 @@ per env (include/pokegym_amd.h `pk_info_ptr`, layout [PK_INFO_NFIELDS][npad]) an
 env's flag (`pk_info_flag_ptr`).  The record holds every numeric scalar of the reference's
 info["stats"] and info["reward"] dicts, in the order below (`levels` as its six raw entries).
 
-One deliberate difference: for an empty party the reference's "highest_pokemon_level"
-(max(party_levels), :1672) raises ValueError and kills the env; the record holds 0 instead.
+For an empty party the reference's "highest_pokemon_level" (max(party_levels), :1672) raises
+ValueError while it builds the dict; the device then records PK_ERR_EMPTY_PARTY for the env (no
+record), and Environment / VecEnv raise ValueError as the reference does.
 
 "coord" (np.sum of the 444x436 counts_map heat map, :648-679) is in the record when the heat map
 is kept (PK_F_HEATMAP; NaN otherwise); the map itself ("pokemon_exploration_map") is a device

@@ -149,7 +149,7 @@ def mutate(w, h, rng, dims, allow_errors):
         _set(w, 0xD803, _get(w, 0xD803) | 1)
 
 
-SC_NONE, SC_KEYERROR, SC_STUCK, SC_CUTCOORDS, SC_HEATMAP = 0, 1, 2, 3, 4
+SC_NONE, SC_KEYERROR, SC_STUCK, SC_CUTCOORDS, SC_HEATMAP, SC_EMPTYPARTY = 0, 1, 2, 3, 4, 5
 
 
 def _scenario(w, t, k, scenario, coords):
@@ -170,6 +170,9 @@ def _scenario(w, t, k, scenario, coords):
                 row = [(0x52, 255, 1, 0, 1, 1), (0x52, 255, 1, 0, 1, 1), (0x52, 1, 1, 0, 1, 1)][t - k]
                 for a, v in zip(CUT_ADDRS, row):
                     _set(w, a, v)
+    elif scenario == SC_EMPTYPARTY and t >= k:
+        for j in range(6):                         # every party level 0 from step k on: the info
+            _set(w, 0xD18C + 44 * j, 0)            # dict of the next done step takes max([])
     elif scenario == SC_HEATMAP and t == k:
         m = max((m for m in coords if m <= 247), key=lambda m: coords[m][1])
         _set(w, 0xD35E, m)

@@ -2,18 +2,25 @@
 
 BASELINE.json's north_star asks for bit-exact WRAM over 10k scripted steps, and the reference's
 only benchmark is 10,000 x step(0) (/root/reference/test.py:16-29).  Timing bugs (DIV-mixing RNG,
-folded LCD events, HALT skip-ahead) grow with the horizon, so this compares the WHOLE machine
-state (v9 savestate digest: WRAM, VRAM, OAM, HRAM, IO, CPU/LCD/timer/MBC registers, clocks, the
-rendered screen) every 250 env-steps along 64 trajectories of 10,000 steps each from power-on:
-trajectory 0 presses Down every step (test.py's a_t = 0), trajectory 1 the [0,3,1,2] cycle of
-configs[1], trajectories 2..63 seeded random presses 0..8 (8 = no button).
+folded LCD events, HALT skip-ahead, fused instruction pairs) grow with the horizon, so this
+compares the WHOLE machine state (v9 savestate digest: WRAM, VRAM, OAM, HRAM, IO, CPU/LCD/timer/
+MBC registers, clocks, the rendered screen) every 250 env-steps along 64 trajectories of 10,000
+steps each from power-on: trajectory 0 presses Down every step (test.py's a_t = 0), trajectory 1
+the [0,3,1,2] cycle of configs[1], trajectories 2..63 seeded random presses 0..8 (8 = no button).
 
 The 10,000 steps of a trajectory are split into 8 segments of 1,250 that run side by side in one
 512-env launch: segment k starts from the oracle's own v9 state at step 1,250k (pk_load_env) —
-so the device is checked continuously over every step of the 10k horizon while the wall time is
-that of 1,250 steps (a single 24-frame env-step is latency-bound at ~65 ms however few envs run).
-Segment 0 starts from power-on on both sides.  tools/horizon_continuous.py runs the same
-trajectories as ONE continuous 10k-step device run (profiles/r02_horizon_continuous.log)."""
+so the device is checked over every step of the 10k horizon, each segment a continuous run of
+1,250 device steps, while the wall time is that of 1,250 steps.  Segment 0 starts from power-on on
+both sides.  The run is repeated for each K1 launch shape the benchmark uses (SHAPES): the small-
+launch shape (256-thread workgroups, one 32-env wave per SIMD, no wave priority) and the
+benchmarked 512-thread workgroups with the wave-priority kernel, pk_step_kernel<true>, at 16 and
+32 envs per wave (configs[3]/[4]'s 32,768-env shard and configs[2]'s 65,536 envs).
+
+test_horizon_65536_envs runs configs[2]'s own launch (65,536 envs) continuously for 240 steps and
+compares one env of every workgroup with the oracle."""
+import os
+
 import numpy as np
 import pytest
 
@@ -25,6 +32,8 @@ pytestmark = pytest.mark.gpu
 TOTAL, SEGS, EVERY, NTRAJ = 10000, 8, 250, 64
 SEG = TOTAL // SEGS
 PARTS = SEG // EVERY
+# K1 launch shapes: (PK_WAVE_LANES, PK_K1_BLOCK); (None, None) = what the handle picks for 512 envs
+SHAPES = {"auto": (None, None), "wg512_l16": ("16", "512"), "wg512_l32": ("32", "512")}
 
 
 def horizon_actions(total=TOTAL, ntraj=NTRAJ) -> np.ndarray:
@@ -34,23 +43,48 @@ def horizon_actions(total=TOTAL, ntraj=NTRAJ) -> np.ndarray:
     return a
 
 
+def _with_shape(shape, fn):
+    """Call fn() with the K1 shape environment of `shape` (read by pk_create)."""
+    lanes, block = SHAPES[shape]
+    old = {k: os.environ.get(k) for k in ("PK_WAVE_LANES", "PK_K1_BLOCK")}
+    try:
+        for k, v in (("PK_WAVE_LANES", lanes), ("PK_K1_BLOCK", block)):
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 @pytest.fixture(scope="module")
-def horizon():
-    import torch
-    from pokegym_amd.emulator import BatchedEmulator
+def oracle_horizon():
     from pokegym_amd.testrom.game import game_rom
     rom = game_rom()
     actions = horizon_actions()
     with OP.pool() as ex:
         dig, keep = OP.trajectories(ex, rom, None, actions, every=EVERY, keep_every=SEG, chunk=4)
-    emu = BatchedEmulator(rom, SEGS * NTRAJ, render=True)
+    return rom, actions, dig, keep
+
+
+@pytest.fixture(scope="module", params=list(SHAPES))
+def horizon(request, oracle_horizon):
+    import torch
+    from pokegym_amd.emulator import BatchedEmulator
+    rom, actions, dig, keep = oracle_horizon
+    emu = _with_shape(request.param, lambda: BatchedEmulator(rom, SEGS * NTRAJ, render=True))
     for k in range(1, SEGS):
         for j in range(NTRAJ):
             emu.load_env(k * NTRAJ + j, keep[(k, j)])
     # device action table: env k*64+j at local step t plays actions[k*SEG + t, j]
     table = np.concatenate([actions[k * SEG:(k + 1) * SEG] for k in range(SEGS)], axis=1)
     st = {"emu": emu, "acts": torch.from_numpy(np.ascontiguousarray(table)).to(emu.device), "dig": dig, "t": 0,
-          "ok": True}
+          "ok": True, "shape": request.param}
     yield st
     emu.close()
 
@@ -74,8 +108,40 @@ def test_horizon_10k_segments(horizon, part):
         want = st["dig"][step // EVERY - 1]
         for j in np.nonzero(got[k] != want)[0]:
             bad.append((int(step), int(j)))
-    assert not bad, f"{len(bad)} (step, trajectory) checkpoints differ: {bad[:8]}"
+    assert not bad, f"[{st['shape']}] {len(bad)} (step, trajectory) checkpoints differ: {bad[:8]}"
     st["ok"] = True
+
+
+def test_horizon_65536_envs():
+    """configs[2]'s benchmarked launch (65,536 envs: 512-thread workgroups, 32-env waves, the
+    wave-priority kernel) stepped continuously for 240 random-action steps; one env of every
+    workgroup (a different lane position in each) is compared with the oracle every 80 steps."""
+    import torch
+    from pokegym_amd.emulator import BatchedEmulator
+    from pokegym_amd.testrom.game import game_rom
+    rom, n, steps, every = game_rom(), 65536, 240, 80
+    per_wg = 256                                     # 8 waves x 32 envs per 512-thread workgroup
+    sample = np.array([g * per_wg + (g * 37) % per_wg for g in range(n // per_wg)])
+    actions = np.random.default_rng(240).integers(0, 8, (steps, n), dtype=np.uint8)
+    with OP.pool() as ex:
+        futs = [(e0, ex.submit(OP._trajectory, rom, None, np.ascontiguousarray(actions[:, sample[e0:e0 + 8]]),
+                               every, steps)) for e0 in range(0, len(sample), 8)]
+        emu = BatchedEmulator(rom, n, render=True)
+        acts = torch.from_numpy(actions).to(emu.device)
+        got = np.zeros((steps // every, len(sample)), np.uint64)
+        for t in range(steps):
+            emu.step(acts[t])
+            if (t + 1) % every == 0:
+                torch.cuda.synchronize()
+                st = np.stack([emu.snapshot_range(int(e), 1)[0] for e in sample])
+                got[(t + 1) // every - 1] = oracle.state_digests(st)
+        emu.close()
+        want = np.zeros_like(got)
+        for e0, f in futs:
+            d, _ = f.result()
+            want[:, e0:e0 + d.shape[1]] = d
+    bad = [(int((k + 1) * every), int(sample[j])) for k, j in zip(*np.nonzero(got != want))]
+    assert not bad, f"{len(bad)} (step, env) checkpoints differ: {bad[:8]}"
 
 
 def test_horizon_64_bank_rom():

@@ -34,7 +34,8 @@ from pokegym_amd import reward_tables as T  # noqa: E402
 SEQUENCES = ([(s, 60, 20480, 0, 0) for s in range(40)]
              + [(100 + s, 50, 17, 0, 0) for s in range(8)]
              + [(200 + s, 60, 20480, 1, 0) for s in range(16)]
-             + [(300 + s, 20, 20480, 0, sc) for s in range(2) for sc in (1, 2, 3, 4)])
+             + [(300 + s, 20, 20480, 0, sc) for s in range(2) for sc in (1, 2, 3, 4)]
+             + [(400 + s, 20, 12 + s, 0, 5) for s in range(2)])
 
 
 def obs_hash(o):
