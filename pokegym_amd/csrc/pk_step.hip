@@ -44,6 +44,11 @@
 #ifndef PK_ITER
 #define PK_ITER(env, ev) ((void)(ev))
 #endif
+// every active lane of the wave holds the same value (the host simulation runs one lane per
+// thread and picks the path with pk_sim_uniform)
+#ifndef PK_WAVE_UNIFORM
+#define PK_WAVE_UNIFORM(v) (__builtin_amdgcn_ballot_w64((v) != __builtin_amdgcn_readfirstlane(v)) == 0ull)
+#endif
 #ifndef PK_ITER_OP
 #define PK_ITER_OP(env, di) ((void)0)
 #endif
@@ -381,6 +386,219 @@ __device__ __forceinline__ void pk_write_slow(const PkStepArgs* A, u8* g, u32 la
 }
 
 // ---------------------------------------------------------------------------------------------
+// One emulated instruction's execution: address, operand reads, fused datapath, control
+// (pk_exec) and memory writes (pk_write).  UNI: every active lane of the wave holds the same
+// microcode entry (the loop tests it each iteration; configs[1]'s lockstep envs, episode starts
+// from one savestate, wake-ups at VBlank), so sD/sU/sK — the entry's D/U/K words read into
+// scalar registers — steer scalar branches that skip the datapath units, the address and the
+// memory stages the instruction does not use.  !UNI: the straight-line all-units form.
+struct Mc {   // a microcode entry (pk_ucode.h), one VGPR per word
+    u32 D, U, K, V, XR, XE, YR, YE, AR, AE, S0, S1, YC, YX, CW, CI;
+};
+struct Ex {   // what the rest of the iteration needs from the instruction
+    u32 addr0, addr1, o0, o1, wv0, wv1, cycles;
+    bool wr, wr2, wram;
+};
+#define PK_DM_MEM ((1u << PK_DB_RD) | (1u << PK_DB_WR))
+// the flags change: F bits other than the kept ones, or POP AF
+__device__ __forceinline__ bool uc_flags(u32 K, u32 U) {
+    return ((K >> 8) & 0xFFu) != 0xF0u || ((K >> 16) & 0xFFu) != 0u || (U & (1u << PK_US_FPOP)) != 0u;
+}
+
+template <bool UNI, bool PRIO>
+__device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, const Mc& m, u32 sD, u32 sU, u32 sK,
+                                        u32& ev, Ex& x) {
+    const PkStepArgs& A = *c.A;
+    const u32 D = m.D, U = m.U, K = m.K;
+    // ---------------- operands, condition, memory address ----------------
+    const u32 w0 = s.w0, w1 = s.w1, sp = s.sp;
+    const u32 F = (w1 >> 16) & 0xFFu;
+    const u32 pcn = (pc + (D & 3u)) & 0xFFFFu;
+    const u32 taken = (((F | 0x100u) >> ((D >> PK_DB_CPOS) & 15u)) & 1u) ^ bit(D, PK_DB_CINV);
+    u32 addr0 = 0, addr1 = 0, o0 = 0, o1 = 0;
+    bool pair = false, fast01 = false;
+    if (!UNI || (sD & PK_DM_MEM)) {
+        // operand pools: registers (w1:w0) and ext (q1:q0) = instruction bytes, m0|m1 and SP
+        const u32 asrc = perm(w1, w0, m.AR) | perm(sp << 16, bytes, m.AE);
+        addr0 = (asrc + (u32)sfield(D, PK_DB_AOFF, 2)) & 0xFFFFu;
+        addr1 = (addr0 + (u32)sfield(D, PK_DB_ADIR, 2)) & 0xFFFFu;
+        // image offsets of both addresses, shared by the fast read and write paths
+        // The fast paths take a pair (addr1 = addr0 + ADIR, ADIR in -1/0/+1) only inside one
+        // 512-byte block of plain RAM, where fast_phys is linear: o1 follows from o0.  A pair that
+        // crosses a block boundary (incl. WRAM/echo at 0xE000 and echo/OAM at 0xFE00) is rare
+        // and goes through the generic bus paths.
+        o0 = fast_phys(addr0) * PK_LANES + c.lane;
+        o1 = o0 + (u32)(sfield(D, PK_DB_ADIR, 2) * (int)PK_LANES);
+        pair = ((addr0 ^ addr1) & 0xFE00u) == 0u;  // both in one 512-byte block
+        fast01 = fast_ram(addr0) & fast_ram(addr1) & pair;
+    }
+
+    // ---------------- memory reads (m0 at addr0, m1 at addr1) ----------------
+    const bool rd = bit(D, PK_DB_RD) != 0u, rd2 = bit(D, PK_DB_RD2) != 0u;
+    u32 m16 = 0;
+    if (!UNI || (sD & (1u << PK_DB_RD))) {
+        const bool rram = rd & fast01;  // addr1 == addr0 for 1-byte reads
+        // staged ROM is 16 KB-aligned: inside one block addr1 is staged iff addr0 is, at index + ADIR
+        const bool rrom = rd & rom_staged(s, addr0) & pair;
+        // each source has its own result registers, merged by OR below: sharing one register
+        // would make the LDS ROM read wait for the image load of other lanes (write-after-write)
+        u32 rm0 = 0, rm1 = 0, om0 = 0, om1 = 0, xm = 0;
+        if (rram) {
+            rm0 = c.g[o0];
+            if (rd2) rm1 = c.g[o1];
+        }
+        if (rrom) {
+            const u32 i0 = rom_lds_index(s, addr0);
+            om0 = lds_rom[i0];
+            om1 = lds_rom[i0 + (u32)sfield(D, PK_DB_ADIR, 2)];  // == om0 for 1-byte reads
+        }
+        if (PK_RARE(rd & !rram & !rrom)) {  // rare: IO registers (LY, STAT, joypad, ...), SRAM, unstaged ROM
+            PK_STAMP_AT(0);
+            if (!rd2 & (addr0 >= 0xFF00u) & ((addr0 < 0xFF80u) | (addr0 == 0xFFFFu))) {
+                xm = io_read(c, s, addr0);
+                ev |= PK_EV_RD_IO;
+            } else if ((addr0 - 0x4000u < 0x4000u) & pair) {  // unstaged switchable bank: the global ROM
+                const u32 ga = rom_global_index(A, s, addr0);
+                xm = A.rom[ga] | sel(rd2, (u32)A.rom[ga + (u32)sfield(D, PK_DB_ADIR, 2)] << 8, 0u);
+                ev |= PK_EV_RD_ROMG;
+            } else {
+                const St t = s;
+                xm = pk_read_slow(&A, c.g, c.lane, c.loc, &t, addr0, addr1, rd2 ? 1u : 0u);
+                ev |= PK_EV_RD_ROMG;
+            }
+            PK_STAMP_AT(1);
+        }
+        // m0 | m1 << 8 (m1 is only meaningful for two-byte reads: one-byte operands select m0 alone)
+        m16 = rm0 | om0 | xm | ((rm1 | om1) << 8);
+        ev |= sel(rd, PK_EV_RD | sel(rd2, PK_EV_RD2, 0u) | sel(rram, PK_EV_RD_RAM, 0u) | sel(rrom, PK_EV_RD_ROMLDS, 0u)
+                      | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
+                      | sel(addr0 >= 0xC000u && addr0 < 0xFE00u, PK_EV_RD_WRAM, 0u), 0u);
+    }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);   // operand read issued: the SIMD's other wave first
+    PK_STAMP_AT(0);
+
+    // ---------------- fused datapath ----------------
+    const u32 q1 = m16 | (sp << 16);
+    const u32 X = perm(w1, w0, m.XR) | perm(q1, bytes, m.XE);
+    const u32 Y = perm(w1, w0, m.YR) | perm(q1, bytes, m.YE) | m.YC;
+    const bool right = bit(U, PK_US_RIGHT) != 0u;
+    u32 cin = 0, r = 0, cvx = 0, rs = 0, lres = 0;
+    // carry-in of the adder, or the bit shifted in by the right-shift unit: bit CW of
+    // (X | F << 16) ^ CI (F.C at bit 20, X's bits 7/0, bit 16 = 0 for the constants)
+    if (!UNI || (sU & ((1u << PK_US_ADD) | (1u << PK_US_RIGHT))))
+        cin = ((((X & 0xFFFFu) | (w1 & 0xFFFF0000u)) ^ m.CI) & m.CW) != 0u ? 1u : 0u;
+    // adder: r = X + Y ^ YX + cin (YX = 0x1FFFF subtracts); X ^ Y ^ r = the carry (borrow) into
+    // each bit.  Left rotates and shifts are X + X + (0 / F.C / bit 7): bit 8 is the carry out
+    if (!UNI || (sU & (1u << PK_US_ADD))) {
+        r = X + (Y ^ m.YX) + cin;
+        cvx = X ^ Y ^ r;
+    }
+    // right-shift unit: RRC RRA RR SRA SRL ((X | in << 8 | X.0 << 9) >> 1: bit 8 = the bit
+    // shifted out) and SWAP ((X | X << 8) >> 4)
+    if (!UNI || (sU & (1u << PK_US_RIGHT))) {
+        const bool swap = bit(U, PK_US_SWAP) != 0u;
+        rs = (X | (sel(swap, X, cin | ((X & 1u) << 1)) << 8)) >> sel(swap, 4u, 1u);
+    }
+    // logic: (X & Y) and/or (X ^ Y) (OR = both); loads are 0xFF AND Y
+    if (!UNI || (sU & (1u << PK_US_LOGIC)))
+        lres = ((X & Y) & (u32)sfield(U, PK_US_LAND, 1)) | ((X ^ Y) & (u32)sfield(U, PK_US_LXOR, 1));
+    u32 res8 = sel(bit(U, PK_US_LOGIC), lres, sel(right, rs, r)) & 0xFFu;
+    // flags: F' = (F & FK) | ((Z | H | C | FC) & FM), H/C = carry bits 4/8 (12/16 for ADD HL) or
+    // the right unit's shifted-out bit 8
+    u32 nf = F;
+    const bool fchg = !UNI || uc_flags(sK, sU);
+    if (fchg) {
+        const u32 cs = sel(right, rs, cvx) >> (bit(U, PK_US_HSH8) * 8u);
+        const u32 fv = sel(res8 == 0u, 0x80u, 0u) | ((cs << 1) & 0x20u) | ((cs >> 4) & 0x10u) | K;
+        nf = ((F & (K >> 8)) | (fv & (K >> 16))) & 0xFFu;
+        nf = sel(bit(U, PK_US_FPOP), m16 & 0xF0u, nf);
+    }
+    if (PK_RARE(bit(D, PK_DB_DAA))) {  // DAA (opcodes.py DAA_27), rare
+        const u32 a = w1 >> 24;
+        u32 corr = sel(F & 0x20u, 0x06u, 0u) | sel(F & 0x10u, 0x60u, 0u);
+        corr |= sel(F & 0x40u, 0u, sel((a & 0x0Fu) > 0x09u, 0x06u, 0u) | sel(a > 0x99u, 0x60u, 0u));
+        res8 = sel(F & 0x40u, a - corr, a + corr) & 0xFFu;
+        nf = (F & 0x40u) | sel(res8 == 0u, 0x80u, 0u) | sel(corr & 0x60u, 0x10u, 0u);
+    }
+    // register writeback: val = res16 | F' << 16 | res8 << 24 through the per-op byte selectors
+    // (res16: the adder, or HL +- 1 for (HL+)/(HL-); bytes 2-3 of either are not taken)
+    const u32 u16 = sel(bit(U, PK_US_R16HL), w1 + (u32)sfield(U, PK_US_HLINC, 2), r);
+    if (!UNI || fchg || (sU & (1u << PK_US_REGW))) {
+        const u32 val = perm(nf | (res8 << 8), u16, 0x05040100u);
+        s.w0 = perm(val, w0, m.S0);
+        s.w1 = perm(val, w1, m.S1);
+    }
+
+    // ---------------- control transfer, SP, IME/HALT ----------------
+    // JP/CALL/INT nn, JP HL, RET, RST: X | Y (one of them is 0); JR: pc + 2 + (Y = sext e)
+    s.pc = pcn;
+    if (!UNI || (sU & (1u << PK_US_JUMP))) {
+        const u32 tgt = (X + Y + (pcn & m.V)) & 0xFFFFu;
+        const bool jump = bit(U, PK_US_JUMP) != 0u && taken != 0u;
+        s.pc = sel(jump, tgt, pcn);
+        ev |= sel(jump, PK_EV_JUMP, 0u);
+    }
+    x.cycles = ((D >> PK_DB_CYC) & 7u) * 4u + sel(taken != 0u, ((D >> PK_DB_XCYC) & 3u) * 4u, 0u);
+    if (!UNI || (sU & ((1u << PK_US_SPW) | (7u << PK_US_SPD)))) {
+        const u32 sp2 = (sp + ((u32)sfield(U, PK_US_SPD, 3) & (0u - taken))) & 0xFFFFu;
+        s.sp = sel(bit(U, PK_US_SPW), u16 & 0xFFFFu, sp2);
+    }
+    // IME / HALT / CRASH / QUEUED: (cpu & keep) | set from the microcode
+    s.cpu = (s.cpu & (0xFFFFFFF0u | ((K >> 24) & 15u))) | (K >> 28);
+
+    // the write: wv0 at addr0, wv1 at addr1 (16-bit writes: low byte first in memory; pushes
+    // SP-2, SP-1); the stage itself (pk_write) runs after the secondary op
+    x.wr = bit(D, PK_DB_WR) != 0u && taken != 0u;
+    x.wr2 = bit(D, PK_DB_WR2) != 0u;
+    x.wram = x.wr & fast01;
+    const u32 wv = sel(bit(U, PK_US_W16), sel(bit(U, PK_US_WPC), pcn, X), res8);
+    x.wv0 = wv & 0xFFu;
+    x.wv1 = (wv >> 8) & 0xFFu;
+    x.addr0 = addr0;
+    x.addr1 = addr1;
+    x.o0 = o0;
+    x.o1 = o1;
+}
+
+template <bool UNI>
+__device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc& m, u32 sD, const Ex& x, u32& ev) {
+    const PkStepArgs& A = *c.A;
+    if (UNI && !(sD & (1u << PK_DB_WR))) return;
+    if (x.wram) {
+        // VRAM / OAM change while rendered lines are pending: rasterise them first (rare)
+        // (lines are pending only in the rendered frame: test that first, alone)
+        if (PK_RARE(s.npend != 0u)) {
+            PK_STAMP_AT(2);
+            if (vram_or_oam(x.addr0) | (x.wr2 & vram_or_oam(x.addr1))) {
+                PK_STAMP_AT(11);
+                flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, env, c.gid);
+                PK_STAMP_AT(10);
+                s.npend = 0;
+                ev |= PK_EV_FLUSH;
+            }
+        }
+        c.g[x.o0] = (u8)x.wv0;
+        hcode_st(c, x.addr0, x.wv0);
+        if (x.wr2) {
+            c.g[x.o1] = (u8)x.wv1;
+            hcode_st(c, x.addr1, x.wv1);
+        }
+    }
+    PK_STAMP_AT(2);
+    if (PK_RARE(x.wr & !x.wram)) {  // rare: IO registers / MBC / SRAM / OAM DMA / IE
+        St t = s;
+        pk_write_slow(&A, c.g, c.lane, c.loc, env, c.gid, &t, x.addr0, x.wv0, x.addr1, x.wv1, x.wr2 ? 1u : 0u,
+                      bit(m.U, PK_US_HIFIRST));
+        s = t;
+        ev |= PK_EV_WR_SLOW;
+        PK_STAMP_AT(3);
+    }
+    ev |= sel(x.wr, PK_EV_WR | sel(x.wr2, PK_EV_WR2, 0u) | sel(x.addr0 >= 0xFF80u && x.addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
+                        | sel(x.addr0 >= 0xC000u && x.addr0 < 0xFE00u, PK_EV_WR_WRAM,
+                              sel(x.addr0 >= 0x8000u && x.addr0 < 0xA000u, PK_EV_WR_VRAM, 0u)), 0u);
+}
+
+// ---------------------------------------------------------------------------------------------
 // K1
 // PRIO: the launch runs two waves per SIMD (A.prio, chosen by the host), and K1 raises a wave's
 // issue priority over its dependent fetch -> decode -> operand-read chain (see the prefetch stage)
@@ -464,7 +682,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
     // software pipeline: the next instruction's bytes and microcode entry, loaded from LDS at the
     // end of the previous iteration (after its writes, so bank switches and HRAM code stores are
     // seen) while the timer/LCD work runs; pf = 0 -> fetch and decode at the top instead
-    u32 pf = 0, pbytes = 0;
+    u32 pf = 0, pbytes = 0, pdi = 0;   // pdi: the prefetched microcode index
     uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0, p2 = p0, p3 = p0;
 #ifdef PK_STAMP
     uint64_t st_acc[PK_NSTAMP] = {}, st_prev = __builtin_amdgcn_s_memtime(), st_iter = 0;
@@ -496,7 +714,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         }
 
         // ---------------- fetch + microcode entry (prefetched, or here when pf = 0) ----------------
-        u32 bytes = pbytes;
+        u32 bytes = pbytes, cdi = pdi;
         uint4 e0 = p0, e1 = p1, e2 = p2, e3 = p3;
         if (PK_RARE(!pf)) {
             PK_STAMP_AT(8);
@@ -536,126 +754,26 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             e1 = ucv[di * 4u + 1u];
             e2 = ucv[di * 4u + 2u];
             e3 = ucv[di * 4u + 3u];
+            cdi = di;
             PK_STAMP_AT(9);
         }
         icount += sel(exec, 1u, 0u);
         ev |= sel(exec, PK_EV_EXEC | sel((bytes & 0xFFu) == 0xCBu, PK_EV_CB, 0u), 0u) | sel(pf != 0u, PK_EV_F_LDS, 0u)
             | sel(dispatch, PK_EV_INT, 0u) | sel(!exec && !dispatch, PK_EV_IDLE, 0u);
         if (exec) PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, bytes & 0xFFu);
-        const u32 D = e0.x, U = e0.y, K = e0.z, V = e0.w, XR = e1.x, XE = e1.y, YR = e1.z, YE = e1.w, AR = e2.x, AE = e2.y,
-                  S0 = e2.z, S1 = e2.w, YC = e3.x, YX = e3.y, CW = e3.z, CI = e3.w;
-
-        // ---------------- operands, condition, memory address ----------------
-        const u32 w0 = s.w0, w1 = s.w1, sp = s.sp;
-        const u32 F = (w1 >> 16) & 0xFFu;
-        const u32 pcn = (pc + (D & 3u)) & 0xFFFFu;
-        const u32 taken = (((F | 0x100u) >> ((D >> PK_DB_CPOS) & 15u)) & 1u) ^ bit(D, PK_DB_CINV);
-        // operand pools: registers (w1:w0) and ext (q1:q0) = instruction bytes, m0|m1 and SP
-        const u32 asrc = perm(w1, w0, AR) | perm(sp << 16, bytes, AE);
-        const u32 addr0 = (asrc + (u32)sfield(D, PK_DB_AOFF, 2)) & 0xFFFFu;
-        const u32 addr1 = (addr0 + (u32)sfield(D, PK_DB_ADIR, 2)) & 0xFFFFu;
-        // image offsets of both addresses, shared by the fast read and write paths
-        // The fast paths take a pair (addr1 = addr0 + ADIR, ADIR in -1/0/+1) only inside one
-        // 512-byte block of plain RAM, where fast_phys is linear: o1 follows from o0.  A pair that
-        // crosses a block boundary (incl. WRAM/echo at 0xE000 and echo/OAM at 0xFE00) is rare
-        // and goes through the generic bus paths.
-        const u32 o0 = fast_phys(addr0) * PK_LANES + c.lane;
-        const u32 o1 = o0 + (u32)(sfield(D, PK_DB_ADIR, 2) * (int)PK_LANES);
-        const bool pair = ((addr0 ^ addr1) & 0xFE00u) == 0u;  // both in one 512-byte block
-        const bool fast01 = fast_ram(addr0) & fast_ram(addr1) & pair;
-
-        // ---------------- memory reads (m0 at addr0, m1 at addr1) ----------------
-        const bool rd = bit(D, PK_DB_RD) != 0u, rd2 = bit(D, PK_DB_RD2) != 0u;
-        const bool rram = rd & fast01;  // addr1 == addr0 for 1-byte reads
-        // staged ROM is 16 KB-aligned: inside one block addr1 is staged iff addr0 is, at index + ADIR
-        const bool rrom = rd & rom_staged(s, addr0) & pair;
-        // each source has its own result registers, merged by OR below: sharing one register
-        // would make the LDS ROM read wait for the image load of other lanes (write-after-write)
-        u32 rm0 = 0, rm1 = 0, om0 = 0, om1 = 0, xm = 0;
-        if (rram) {
-            rm0 = c.g[o0];
-            if (rd2) rm1 = c.g[o1];
+        const Mc m = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y, e2.z, e2.w, e3.x, e3.y, e3.z, e3.w};
+        const u32 D = m.D;
+        // ---------------- execute: uniform (one microcode entry in every lane) or general ----------------
+        Ex x;
+        if (PK_WAVE_UNIFORM(cdi)) {
+            const u32 sD = __builtin_amdgcn_readfirstlane(m.D), sU = __builtin_amdgcn_readfirstlane(m.U),
+                      sK = __builtin_amdgcn_readfirstlane(m.K);
+            pk_exec<true, PRIO>(s, c, pc, bytes, m, sD, sU, sK, ev, x);
+        } else {
+            pk_exec<false, PRIO>(s, c, pc, bytes, m, m.D, m.U, m.K, ev, x);
         }
-        if (rrom) {
-            const u32 i0 = rom_lds_index(s, addr0);
-            om0 = lds_rom[i0];
-            om1 = lds_rom[i0 + (u32)sfield(D, PK_DB_ADIR, 2)];  // == om0 for 1-byte reads, masked below
-        }
-        if (PK_RARE(rd & !rram & !rrom)) {  // rare: IO registers (LY, STAT, joypad, ...), SRAM, unstaged ROM
-            PK_STAMP_AT(0);
-            if (!rd2 & (addr0 >= 0xFF00u) & ((addr0 < 0xFF80u) | (addr0 == 0xFFFFu))) {
-                xm = io_read(c, s, addr0);
-                ev |= PK_EV_RD_IO;
-            } else if ((addr0 - 0x4000u < 0x4000u) & pair) {  // unstaged switchable bank: the global ROM
-                const u32 ga = rom_global_index(A, s, addr0);
-                xm = A.rom[ga] | sel(rd2, (u32)A.rom[ga + (u32)sfield(D, PK_DB_ADIR, 2)] << 8, 0u);
-                ev |= PK_EV_RD_ROMG;
-            } else {
-                const St t = s;
-                xm = pk_read_slow(&A, c.g, c.lane, c.loc, &t, addr0, addr1, rd2 ? 1u : 0u);
-                ev |= PK_EV_RD_ROMG;
-            }
-            PK_STAMP_AT(1);
-        }
-        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);   // operand read issued: the SIMD's other wave first
-        // m0 | m1 << 8 (m1 is only meaningful for two-byte reads: one-byte operands select m0 alone)
-        const u32 m16 = rm0 | om0 | xm | ((rm1 | om1) << 8);
-        ev |= sel(rd, PK_EV_RD | sel(rd2, PK_EV_RD2, 0u) | sel(rram, PK_EV_RD_RAM, 0u) | sel(rrom, PK_EV_RD_ROMLDS, 0u)
-                      | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
-                      | sel(addr0 >= 0xC000u && addr0 < 0xFE00u, PK_EV_RD_WRAM, 0u), 0u);
-        PK_STAMP_AT(0);
-
-        // ---------------- fused datapath ----------------
-        const u32 q1 = m16 | (sp << 16);
-        const u32 X = perm(w1, w0, XR) | perm(q1, bytes, XE);
-        const u32 Y = perm(w1, w0, YR) | perm(q1, bytes, YE) | YC;
-        // carry-in of the adder, or the bit shifted in by the right-shift unit: bit CW of
-        // (X | F << 16) ^ CI (F.C at bit 20, X's bits 7/0, bit 16 = 0 for the constants)
-        const u32 cin = ((((X & 0xFFFFu) | (w1 & 0xFFFF0000u)) ^ CI) & CW) != 0u ? 1u : 0u;
-        // adder: r = X + Y ^ YX + cin (YX = 0x1FFFF subtracts); X ^ Y ^ r = the carry (borrow) into
-        // each bit.  Left rotates and shifts are X + X + (0 / F.C / bit 7): bit 8 is the carry out
-        const u32 r = X + (Y ^ YX) + cin;
-        const u32 cvx = X ^ Y ^ r;
-        // right-shift unit: RRC RRA RR SRA SRL ((X | in << 8 | X.0 << 9) >> 1: bit 8 = the bit
-        // shifted out) and SWAP ((X | X << 8) >> 4)
-        const bool swap = bit(U, PK_US_SWAP) != 0u, right = bit(U, PK_US_RIGHT) != 0u;
-        const u32 rs = (X | (sel(swap, X, cin | ((X & 1u) << 1)) << 8)) >> sel(swap, 4u, 1u);
-        // logic: (X & Y) and/or (X ^ Y) (OR = both); loads are 0xFF AND Y
-        const u32 lres = ((X & Y) & (u32)sfield(U, PK_US_LAND, 1)) | ((X ^ Y) & (u32)sfield(U, PK_US_LXOR, 1));
-        u32 res8 = sel(bit(U, PK_US_LOGIC), lres, sel(right, rs, r)) & 0xFFu;
-        // flags: F' = (F & FK) | ((Z | H | C | FC) & FM), H/C = carry bits 4/8 (12/16 for ADD HL) or
-        // the right unit's shifted-out bit 8
-        const u32 cs = sel(right, rs, cvx) >> (bit(U, PK_US_HSH8) * 8u);
-        const u32 fv = sel(res8 == 0u, 0x80u, 0u) | ((cs << 1) & 0x20u) | ((cs >> 4) & 0x10u) | K;
-        u32 nf = ((F & (K >> 8)) | (fv & (K >> 16))) & 0xFFu;
-        nf = sel(bit(U, PK_US_FPOP), m16 & 0xF0u, nf);
-        if (PK_RARE(bit(D, PK_DB_DAA))) {  // DAA (opcodes.py DAA_27), rare
-            const u32 a = w1 >> 24;
-            u32 corr = sel(F & 0x20u, 0x06u, 0u) | sel(F & 0x10u, 0x60u, 0u);
-            corr |= sel(F & 0x40u, 0u, sel((a & 0x0Fu) > 0x09u, 0x06u, 0u) | sel(a > 0x99u, 0x60u, 0u));
-            res8 = sel(F & 0x40u, a - corr, a + corr) & 0xFFu;
-            nf = (F & 0x40u) | sel(res8 == 0u, 0x80u, 0u) | sel(corr & 0x60u, 0x10u, 0u);
-        }
-        // register writeback: val = res16 | F' << 16 | res8 << 24 through the per-op byte selectors
-        // (res16: the adder, or HL +- 1 for (HL+)/(HL-); bytes 2-3 of either are not taken)
-        const u32 u16 = sel(bit(U, PK_US_R16HL), w1 + (u32)sfield(U, PK_US_HLINC, 2), r);
-        const u32 val = perm(nf | (res8 << 8), u16, 0x05040100u);
-        s.w0 = perm(val, w0, S0);
-        s.w1 = perm(val, w1, S1);
-
-        // ---------------- control transfer, SP, IME/HALT ----------------
-        // JP/CALL/INT nn, JP HL, RET, RST: X | Y (one of them is 0); JR: pc + 2 + (Y = sext e)
-        const u32 tgt = (X + Y + (pcn & V)) & 0xFFFFu;
-        const bool jump = bit(U, PK_US_JUMP) != 0u && taken != 0u;
-        s.pc = sel(jump, tgt, pcn);
-        ev |= sel(jump, PK_EV_JUMP, 0u);
-        u32 cycles = ((D >> PK_DB_CYC) & 7u) * 4u + sel(taken != 0u, ((D >> PK_DB_XCYC) & 3u) * 4u, 0u);
-        const u32 sp2 = (sp + ((u32)sfield(U, PK_US_SPD, 3) & (0u - taken))) & 0xFFFFu;
-        s.sp = sel(bit(U, PK_US_SPW), u16 & 0xFFFFu, sp2);
-        {
-            // IME / HALT / CRASH / QUEUED: (cpu & keep) | set from the microcode
-            s.cpu = (s.cpu & (0xFFFFFFF0u | ((K >> 24) & 15u))) | (K >> 28);
-        }
+        u32 cycles = x.cycles;
+        const bool wr = x.wr, wram = x.wram;
         // ---------------- fused secondary op (pk_ucode.h pk_u2_entry) ----------------
         // The instruction after this one, if it is a JR (cc), LD r,r', INC/DEC r, INC/DEC BC/DE/HL or
         // NOP, runs in this iteration on the registers and flags just written, as PyBoy's next
@@ -666,8 +784,6 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         // it writes no IO/MBC register (slow write).  Code in RAM also needs: no write at all (the
         // fetched bytes stay valid), both instructions within the 3 bytes every fetch path provides
         // (ROM code has 4), and none of them an IO register (DIV and a folded STAT change with the clock).
-        const bool wr = bit(D, PK_DB_WR) != 0u && taken != 0u, wr2 = bit(D, PK_DB_WR2) != 0u;
-        const bool wram = wr & fast01;
         {
             const u32 nxt = bytes >> (8u * (D & 3u));
             const uint4 u2 = ucv2[(nxt & 0xFFu) | (D & (1u << PK_DB_NOFUSE))];
@@ -727,40 +843,8 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         }
 
         // ---------------- memory writes (wv0 at addr0, wv1 at addr1) ----------------
-        // 16-bit writes: low byte at addr0, high byte at addr1 (pushes: SP-2, SP-1)
-        const u32 wv = sel(bit(U, PK_US_W16), sel(bit(U, PK_US_WPC), pcn, X), res8);
-        const u32 wv0 = wv & 0xFFu, wv1 = (wv >> 8) & 0xFFu;
-        if (wram) {
-            // VRAM / OAM change while rendered lines are pending: rasterise them first (rare)
-            // (lines are pending only in the rendered frame: test that first, alone)
-            if (PK_RARE(s.npend != 0u)) {
-                PK_STAMP_AT(2);
-                if (vram_or_oam(addr0) | (wr2 & vram_or_oam(addr1))) {
-                    PK_STAMP_AT(11);
-                    flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, env, c.gid);
-                    PK_STAMP_AT(10);
-                    s.npend = 0;
-                    ev |= PK_EV_FLUSH;
-                }
-            }
-            c.g[o0] = (u8)wv0;
-            hcode_st(c, addr0, wv0);
-            if (wr2) {
-                c.g[o1] = (u8)wv1;
-                hcode_st(c, addr1, wv1);
-            }
-        }
-        PK_STAMP_AT(2);
-        if (PK_RARE(wr & !wram)) {  // rare: IO registers / MBC / SRAM / OAM DMA / IE
-            St t = s;
-            pk_write_slow(&A, c.g, c.lane, c.loc, env, c.gid, &t, addr0, wv0, addr1, wv1, wr2 ? 1u : 0u,
-                          bit(U, PK_US_HIFIRST));
-            s = t;
-            ev |= PK_EV_WR_SLOW;
-            PK_STAMP_AT(3);
-        }
-        ev |= sel(wr, PK_EV_WR | sel(wr2, PK_EV_WR2, 0u) | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
-                      | sel(addr0 >= 0xC000u && addr0 < 0xFE00u, PK_EV_WR_WRAM, sel(addr0 >= 0x8000u && addr0 < 0xA000u, PK_EV_WR_VRAM, 0u)), 0u);
+        if (PK_WAVE_UNIFORM(cdi)) pk_write<true>(s, c, env, m, __builtin_amdgcn_readfirstlane(m.D), x, ev);
+        else pk_write<false>(s, c, env, m, m.D, x, ev);
 
         // ---------------- prefetch the next instruction (LDS-staged ROM or the HRAM mirror) ----------------
         // wave priority (two waves per SIMD): from here through the next iteration's fetch, decode
@@ -791,6 +875,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             p1 = ucv[di * 4u + 1u];
             p2 = ucv[di * 4u + 2u];
             p3 = ucv[di * 4u + 3u];
+            pdi = di;
             pf = sel(fl | fh | fg, 1u, 0u);
         }
 

@@ -49,3 +49,18 @@ def test_hostsim_hram_code():
     """Code fetched from inside, across and outside the LDS-mirrored HRAM bytes, self-modified."""
     from pokegym_amd.testrom.fuzz import hram_code_rom
     assert check(hram_code_rom(), 8, 3, 5) == []
+
+
+@pytest.mark.parametrize("seed", [0, 3, 21, 58])
+def test_hostsim_general_execute_path(seed):
+    """The host simulation runs one lane per thread, so by default every iteration takes K1's
+    wave-uniform execute path (pk_exec<true>: scalar branches around unused units); this runs the
+    general all-units path (pk_exec<false>, what divergent waves execute) against the oracle."""
+    from tests.hostsim import sim
+    L = sim.lib()
+    L.pk_sim_set_uniform(0)
+    try:
+        assert check(fuzz_rom(seed), 8, 3, seed) == []
+        assert check(game_rom(), 4, 4, seed) == []
+    finally:
+        L.pk_sim_set_uniform(1)
