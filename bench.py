@@ -147,6 +147,82 @@ def _stamp(workload: str, rom_tag: str):
     return d, os.path.relpath(path, HERE)
 
 
+class StepFlow:
+    """One env-step of the benchmarked workload over every env of this rank (the timed unit).
+
+    VecEnv workloads (configs[3]): one recv/send of each sub-batch, PufferLib's loop (the
+    sub-batches run on their own streams; VecEnv's logging interval does the sticky-error check and
+    the episode-statistics all-reduce).  Reward workloads (configs[4]): step, episodic-return
+    bookkeeping, the per-env template reload on done and, every `log_every` env-steps, the
+    all-reduce of the episode statistics across ranks (RCCL; gloo in the CPU test of this flow,
+    tests/test_dist.py).  Otherwise a plain step.  `timing` records HIP events around the resets
+    and the all-reduces (GPU only)."""
+
+    def __init__(self, emu, vec, reward, world, log_every, dev, timing=False, warmup_steps=0):
+        import torch
+        self.emu, self.vec, self.reward, self.world, self.log_every = emu, vec, reward, world, log_every
+        self.dev, self.timing = dev, timing
+        self.ep_ret = torch.zeros(emu.n if vec is None else vec.num_envs, dtype=torch.float64, device=dev)
+        self.stats = torch.zeros(3, dtype=torch.float64, device=dev)  # [sum of episodic returns, episodes, resets]
+        self.rst = []      # (start, end) events around each timed reset
+        self.ar_ev = []    # (start, end) events around each timed all-reduce
+        self.allreduces = 0
+        self.global_stats = None   # the last all-reduced copy of stats (every rank holds the same)
+        self.vec_logs = []         # VecEnv logging-interval records (episode statistics, all-reduced)
+
+    def _ev(self):
+        import torch
+        return torch.cuda.Event(enable_timing=True)
+
+    def step(self, t, timed, acts_t=None):
+        import torch
+        import torch.distributed as dist
+        acts_t = self.acts[t] if acts_t is None else acts_t
+        if self.vec is not None:
+            vec = self.vec
+            for _ in range(vec.num_batches):
+                obs, rew, term, trunc, infos, ids, masks = vec.recv()
+                if infos:
+                    self.vec_logs.append(infos[0])
+                vec.send(acts_t[vec.current_envs()])
+            return
+        emu = self.emu
+        obs, rew, term, trunc = emu.step(acts_t)
+        if not self.reward:
+            return
+        d = term.to(torch.float64)
+        self.ep_ret.add_(rew)
+        self.stats[0] += (self.ep_ret * d).sum()
+        self.stats[1] += d.sum()
+        self.ep_ret.mul_(1.0 - d)
+        tm = timed and self.timing
+        if tm:
+            e = (self._ev(), self._ev())
+            e[0].record()
+        emu.reset(term)
+        if tm:
+            e[1].record()
+            self.rst.append(e)
+        if self.world > 1 and t % self.log_every == self.log_every - 1:
+            # configs[4]'s episodic-return all-reduce, every min(128, steps) env-steps
+            if tm:
+                e = (self._ev(), self._ev())
+                e[0].record()
+            glob = self.stats.clone()
+            dist.all_reduce(glob)
+            self.global_stats = glob
+            self.allreduces += 1
+            if tm:
+                e[1].record()
+                self.ar_ev.append(e)
+
+    def reset_ms(self):
+        return sum(a.elapsed_time(b) for a, b in self.rst)
+
+    def allreduce_ms(self):
+        return [a.elapsed_time(b) for a, b in self.ar_ev]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -227,44 +303,9 @@ def main():
                               reload_on_reset=reward, max_episode_steps=max_steps)
         if reward:
             emu.reset()
-    ep_ret = torch.zeros(n, dtype=torch.float64, device=dev)
-    stats = torch.zeros(3, dtype=torch.float64, device=dev)  # [sum of episodic returns, episodes, resets]
-    rst = [torch.cuda.Event(enable_timing=True) for _ in range(2 * (args.warmup + args.steps))]
-    rst_i = [0]
-    ar_ev = []   # (start, end) events around each timed all-reduce (config5 at N>1)
-
-    def env_step(t, timed):
-        if vec is not None:
-            # one env-step of every env = one recv/send of each sub-batch (PufferLib's loop; the
-            # sub-batches run on their own streams, the host never waits)
-            for _ in range(vec.num_batches):
-                obs, rew, term, trunc, infos, ids, masks = vec.recv()
-                vec.send(acts[t, vec.current_envs()])
-            return
-        obs, rew, term, trunc = emu.step(acts[t])
-        if reward:
-            # per-env reload of the template state on done, episodic-return bookkeeping, and the
-            # RCCL all-reduce of the episode statistics every 128 steps (configs[4])
-            d = term.to(torch.float64)
-            ep_ret.add_(rew)
-            stats[0] += (ep_ret * d).sum()
-            stats[1] += d.sum()
-            ep_ret.mul_(1.0 - d)
-            if timed:
-                rst[rst_i[0]].record()
-            emu.reset(term)
-            if timed:
-                rst[rst_i[0] + 1].record()
-                rst_i[0] += 2
-            if world > 1 and t % log_every == log_every - 1:
-                # configs[4]'s episodic-return all-reduce (RCCL), every min(128, steps) env-steps
-                evs = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if timed else None
-                if timed:
-                    evs[0].record()
-                dist.all_reduce(stats)
-                if timed:
-                    evs[1].record()
-                    ar_ev.append(evs)
+    flow = StepFlow(emu, vec, reward, world, log_every, dev, timing=True, warmup_steps=args.warmup + args.steps)
+    stats = flow.stats
+    env_step = flow.step
 
     host_copy = None
     if args.host_obs:
@@ -303,6 +344,7 @@ def main():
     else:
         cyc = torch.tensor([0, 3, 1, 2], dtype=torch.uint8, device=dev)
         acts = cyc[torch.arange(total, device=dev) % 4].unsqueeze(1).expand(total, n).contiguous()
+    flow.acts = acts
     torch.cuda.synchronize(dev)
 
     for t in range(args.warmup):
@@ -327,8 +369,7 @@ def main():
     emu_ms, ren_ms, rew_ms, nprof = emu.profile_read()
     instr = emu.last_instr_count()  # last step's emulated instructions (all envs)
     resets = float(stats[1].item()) - resets0
-    k5_ms = sum(rst[2 * i].elapsed_time(rst[2 * i + 1]) for i in range(rst_i[0] // 2))
-    ar_ms = [a.elapsed_time(b) for a, b in ar_ev]
+    k5_ms, ar_ms = flow.reset_ms(), flow.allreduce_ms()
     # env-steps t (1-based) inside the timed window at which the logging interval fires
     fired = sum(1 for t in range(args.warmup + 1, total + 1) if t % log_every == 0)
     t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)

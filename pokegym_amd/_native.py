@@ -66,6 +66,14 @@ def load(path: str = LIB_PATH):
         raise PkError(f"{path} not found: build it with `python -m pokegym_amd.build` "
                       "(hipcc --offload-arch=gfx950); there is no CPU fallback")
     L = ctypes.CDLL(path)
+    bind(L)
+    _lib = L
+    return L
+
+
+def bind(L):
+    """argtypes of every entry point of include/pokegym_amd.h (shared with the host-simulation
+    test build, tests/hostsim)."""
     u8p = ctypes.POINTER(ctypes.c_uint8)
     vp = ctypes.c_void_p
     L.pk_create.argtypes = [ctypes.POINTER(PkConfig), ctypes.POINTER(vp)]
@@ -89,8 +97,6 @@ def load(path: str = LIB_PATH):
     dp = ctypes.POINTER(ctypes.c_double)
     L.pk_profile_read.argtypes = [vp, dp, dp, dp, ctypes.POINTER(ctypes.c_uint64)]
     bind_v2(L)
-    _lib = L
-    return L
 
 
 def bind_v2(L):
