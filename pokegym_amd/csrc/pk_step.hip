@@ -77,18 +77,21 @@ enum {
 
 // LDS, staged by each workgroup at kernel entry
 __shared__ __attribute__((aligned(16))) u32 lds_uc[PK_UC_WORDS];                  // microcode + secondary ops
-__shared__ __attribute__((aligned(16))) u8 lds_rom[PK_LDS_SLOTS * 0x4000u + 16u]; // ROM banks (+ fetch overrun pad)
-__shared__ int8_t lds_slot[128];                                                  // bank -> slot
+// ROM banks (+ fetch overrun pad), then the HRAM code mirror (below): one byte array, so the
+// next instruction's bytes come from one ds_read2_b32 whichever of the two holds them.
 // Fetch-only mirror of the first PK_HC_ROWS bytes of HRAM (0xFF80-0xFF9F: where games put the
-// OAM-DMA routine, pokered's hDMARoutine included) per env of the workgroup, byte
-// (addr - 0xFF80) * PK_WG_ENVS + local env, + one dummy row: the OAM-DMA wait loop runs from HRAM,
+// OAM-DMA routine, pokered's hDMARoutine included), PK_HC_STRIDE bytes per env of the workgroup
+// at PK_HC_BASE + local env * PK_HC_STRIDE, + one dummy byte: the OAM-DMA wait loop runs from HRAM,
 // and fetching it from the HBM image put a second dependent HBM round trip (fetch, then data) into
 // ~30 % of wave iterations.  Code elsewhere in HRAM is fetched from the image.  Data reads/writes
 // stay on the image (authoritative); every HRAM write also updates the mirror (lanes that do not
-// write a mirrored byte store to the dummy row, so the store needs no branch).  Up to 512 envs per
+// write a mirrored byte store to the dummy byte, so the store needs no branch).  Up to 512 envs per
 // workgroup: 64-env waves two per SIMD when a launch has the envs for it (>= 131,072).
 #define PK_HC_ROWS 32u
-__shared__ u8 lds_hcode[(PK_HC_ROWS + 1u) * PK_WG_ENVS];
+#define PK_HC_STRIDE 36u
+#define PK_HC_BASE (PK_LDS_SLOTS * 0x4000u + 16u)
+__shared__ __attribute__((aligned(16))) u8 lds_rom[PK_HC_BASE + PK_WG_ENVS * PK_HC_STRIDE];
+__shared__ int8_t lds_slot[128];                                                  // bank -> slot
 
 // ---------------------------------------------------------------------------------------------
 // branch-free helpers: arguments are evaluated unconditionally, so ?: on them is a v_cndmask
@@ -131,15 +134,14 @@ __device__ __forceinline__ void st_img(const Ctx& c, u32 phys, u32 v) { c.g[phys
 // keep the HRAM fetch mirror in step with a RAM write at guest address a (row PK_HC_ROWS = dummy)
 __device__ __forceinline__ void hcode_st(const Ctx& c, u32 a, u32 v) {
     const u32 row = sel(a - 0xFF80u < PK_HC_ROWS, a - 0xFF80u, PK_HC_ROWS);
-    lds_hcode[row * PK_WG_ENVS + c.loc] = (u8)v;
+    lds_rom[PK_HC_BASE + c.loc * PK_HC_STRIDE + row] = (u8)v;
 }
 
 // fast RAM: VRAM, WRAM, echo, OAM/unusable, HRAM — plain bytes of the image with no side effects
-__device__ __forceinline__ bool fast_ram(u32 a) {
-    const bool reg = ((0xD0u >> (a >> 13)) & 1u) != 0u;  // regions 0x8000, 0xC000, 0xE000
-    const bool io = a >= 0xFF00u && (a < 0xFF80u || a == 0xFFFFu);
-    return reg && !io;
-}
+__device__ __forceinline__ bool ram_region(u32 a) { return ((0xD0u >> (a >> 13)) & 1u) != 0u; }  // 0x8000, 0xC000, 0xE000
+// IO registers FF00-FF7F and IE (FFFF): a ^ 0x7F maps exactly those to the range FF00-FF80
+__device__ __forceinline__ bool io_addr(u32 a) { return ((a ^ 0x7Fu) - 0xFF00u) <= 0x80u; }
+__device__ __forceinline__ bool fast_ram(u32 a) { return ram_region(a) && !io_addr(a); }
 __device__ __forceinline__ u32 fast_phys(u32 a) {
     const u32 p = (a & 0x1FFFu) + sel(a < 0xA000u, PK_P_VRAM, PK_P_WRAM);
     return sel(a >= 0xFE00u, PK_P_OAM + (a & 0x1FFu), p);
@@ -430,7 +432,8 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
         o0 = fast_phys(addr0) * PK_LANES + c.lane;
         o1 = o0 + (u32)(sfield(D, PK_DB_ADIR, 2) * (int)PK_LANES);
         pair = ((addr0 ^ addr1) & 0xFE00u) == 0u;  // both in one 512-byte block
-        fast01 = fast_ram(addr0) & fast_ram(addr1) & pair;
+        // inside one 512-byte block both addresses share a region; only IO/IE can differ
+        fast01 = ram_region(addr0) & pair & !io_addr(addr0) & !io_addr(addr1);
     }
 
     // ---------------- memory reads (m0 at addr0, m1 at addr1) ----------------
@@ -633,7 +636,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
     c.gid = __builtin_amdgcn_readfirstlane(env / PK_LANES);
     c.g = A.mem + (size_t)c.gid * PK_GROUP_STRIDE;
     c.loc = (threadIdx.x >> 6) * A.wave_lanes + wl;  // < PK_WG_ENVS envs per workgroup
-    for (u32 i = 0; i < PK_HC_ROWS; i++) lds_hcode[i * PK_WG_ENVS + c.loc] = (u8)ld_img(c, PK_P_HRAM + i);
+    for (u32 i = 0; i < PK_HC_ROWS; i++) lds_rom[PK_HC_BASE + c.loc * PK_HC_STRIDE + i] = (u8)ld_img(c, PK_P_HRAM + i);
 
     const u32 np = A.npad;
     u32* R = A.regs;
@@ -725,8 +728,8 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             // image (three loads when pc..pc+2 stay in one 512-byte block of plain RAM), else the bus
             if (PK_RARE(exec & !flds)) {
                 if (pc - 0xFF80u < PK_HC_ROWS - 2u) {  // pc..pc+2 inside the mirrored HRAM bytes
-                    const u32 q = (pc - 0xFF80u) * PK_WG_ENVS + c.loc;
-                    bytes = lds_hcode[q] | (lds_hcode[q + PK_WG_ENVS] << 8) | (lds_hcode[q + 2u * PK_WG_ENVS] << 16);
+                    const u32 q = PK_HC_BASE + c.loc * PK_HC_STRIDE + (pc - 0xFF80u);
+                    bytes = __builtin_amdgcn_alignbyte(romw[(q >> 2) + 1u], romw[q >> 2], q & 3u);
                     ev |= PK_EV_F_BUS | PK_EV_HRAM;
                 } else if (fast_ram(pc) & fast_ram((pc + 2u) & 0xFFFFu) & (((pc ^ (pc + 2u)) & 0xFE00u) == 0u)) {
                     const u32 p = fast_phys(pc);
@@ -855,14 +858,11 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         {
             const u32 npc = s.pc;
             const bool fl = rom_staged(s, npc) && (npc & 0x3FFFu) < 0x3FFEu;
-            const u32 la = sel(fl, rom_lds_index(s, npc), 0u);
-            // staged ROM and the HRAM code mirror are read together, unconditionally (one LDS round
-            // trip; a lane whose pc is not in HRAM reads mirror row 0 and discards it)
+            // staged ROM or the HRAM code mirror: one LDS byte index, one ds_read2_b32
             const bool fh = npc - 0xFF80u < PK_HC_ROWS - 2u;
-            const u32 q = sel(fh, npc - 0xFF80u, 0u) * PK_WG_ENVS + c.loc;
+            const u32 la = sel(fh, PK_HC_BASE + c.loc * PK_HC_STRIDE + (npc - 0xFF80u), sel(fl, rom_lds_index(s, npc), 0u));
             const u32 r0 = romw[la >> 2], r1 = romw[(la >> 2) + 1u];
-            const u32 h0 = lds_hcode[q], h1 = lds_hcode[q + PK_WG_ENVS], h2 = lds_hcode[q + 2u * PK_WG_ENVS];
-            pbytes = sel(fh, h0 | (h1 << 8) | (h2 << 16), __builtin_amdgcn_alignbyte(r1, r0, la & 3u));
+            pbytes = __builtin_amdgcn_alignbyte(r1, r0, la & 3u);
             // code in a switchable bank not staged in LDS (most of a 64-bank cartridge's banks): two
             // dwords of the global ROM (L2-resident), so the microcode entry is still prefetched here
             // and its LDS latency overlaps the timer/LCD stage like that of staged code

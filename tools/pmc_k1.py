@@ -1,5 +1,5 @@
-"""Summarise tools/gpu_pmc_k1.sh passes for K1 (pk_step_kernel): per-wave iteration cost, stall
-split, effective clock.  usage: python tools/pmc_k1.py gpurun_out/pmck_TAG [names...]"""
+"""Summarise tools/gpu_pmc_k1.sh passes for K1 (pk_step_kernel): per-wave cost per emulated
+instruction (issued ISA instructions by class, cycles, waits), effective clock.  usage: python tools/pmc_k1.py gpurun_out/pmck_TAG [names...]"""
 import csv
 import glob
 import json
@@ -32,13 +32,19 @@ def summary(root, name, cus=256):
     bench = json.loads(open(os.path.join(root, f"{name}_a.json")).read().strip().splitlines()[-1])
     waves = c["SQ_WAVES"]
     envs = bench["config"]["envs_per_gpu"]
-    iters = bench["instr_per_env_step"] * 1.09          # loop iterations per wave (HALT/INT overhead ~9 %)
+    # per emulated SM83 instruction of a lane: a wave runs its lanes' instructions side by side, so
+    # wave instructions / (instructions one env executes per launch).  (Round 2 divided by loop
+    # iterations, estimated as 1.09 x instructions; with fused instruction pairs a loop iteration
+    # now executes ~1.37 instructions, so the per-instruction figure is the comparable one: round 2's
+    # rows x 1.09 ~ per-instruction values.)
+    iters = bench["instr_per_env_step"]
     clk = c.get("GRBM_GUI_ACTIVE", 0) / 8 / dur if dur else 0
     per = lambda k: c.get(k, 0) / waves / iters
     out = {
         "name": name, "envs": envs, "waves": waves, "k1_ms": round(dur * 1e3, 2) if dur else None,
         "clock_GHz": round(clk / 1e9, 3),
-        "wave_cycles_per_iter": round(4 * per("SQ_WAVE_CYCLES"), 1),
+        "per": "emulated instruction",
+        "wave_cycles_per_instr": round(4 * per("SQ_WAVE_CYCLES"), 1),
         "active_any": round(4 * per("SQ_ACTIVE_INST_ANY"), 1),
         "wait_any": round(4 * per("SQ_WAIT_ANY"), 1),
         "wait_inst_any": round(4 * per("SQ_WAIT_INST_ANY"), 1),
