@@ -44,11 +44,6 @@
 #ifndef PK_ITER
 #define PK_ITER(env, ev) ((void)(ev))
 #endif
-// every active lane of the wave holds the same value (the host simulation runs one lane per
-// thread and picks the path with pk_sim_uniform)
-#ifndef PK_WAVE_UNIFORM
-#define PK_WAVE_UNIFORM(v) (__builtin_amdgcn_ballot_w64((v) != __builtin_amdgcn_readfirstlane(v)) == 0ull)
-#endif
 #ifndef PK_ITER_OP
 #define PK_ITER_OP(env, di) ((void)0)
 #endif
@@ -389,11 +384,10 @@ __device__ __forceinline__ void pk_write_slow(const PkStepArgs* A, u8* g, u32 la
 
 // ---------------------------------------------------------------------------------------------
 // One emulated instruction's execution: address, operand reads, fused datapath, control
-// (pk_exec) and memory writes (pk_write).  UNI: every active lane of the wave holds the same
-// microcode entry (the loop tests it each iteration; configs[1]'s lockstep envs, episode starts
-// from one savestate, wake-ups at VBlank), so sD/sU/sK — the entry's D/U/K words read into
-// scalar registers — steer scalar branches that skip the datapath units, the address and the
-// memory stages the instruction does not use.  !UNI: the straight-line all-units form.
+// (pk_exec) and memory writes (pk_write), the same straight-line all-units sequence in every lane.
+// (A wave-uniform variant — scalar branches around the units an instruction does not use when
+// every lane holds the same microcode entry — measured slower on every workload, configs[1]'s
+// lockstep envs included: profiles/r03_ab/uniform/.)
 struct Mc {   // a microcode entry (pk_ucode.h), one VGPR per word
     u32 D, U, K, V, XR, XE, YR, YE, AR, AE, S0, S1, YC, YX, CW, CI;
 };
@@ -401,15 +395,8 @@ struct Ex {   // what the rest of the iteration needs from the instruction
     u32 addr0, addr1, o0, o1, wv0, wv1, cycles;
     bool wr, wr2, wram;
 };
-#define PK_DM_MEM ((1u << PK_DB_RD) | (1u << PK_DB_WR))
-// the flags change: F bits other than the kept ones, or POP AF
-__device__ __forceinline__ bool uc_flags(u32 K, u32 U) {
-    return ((K >> 8) & 0xFFu) != 0xF0u || ((K >> 16) & 0xFFu) != 0u || (U & (1u << PK_US_FPOP)) != 0u;
-}
-
-template <bool UNI, bool PRIO>
-__device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, const Mc& m, u32 sD, u32 sU, u32 sK,
-                                        u32& ev, Ex& x) {
+template <bool PRIO>
+__device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, const Mc& m, u32& ev, Ex& x) {
     const PkStepArgs& A = *c.A;
     const u32 D = m.D, U = m.U, K = m.K;
     // ---------------- operands, condition, memory address ----------------
@@ -419,7 +406,7 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     const u32 taken = (((F | 0x100u) >> ((D >> PK_DB_CPOS) & 15u)) & 1u) ^ bit(D, PK_DB_CINV);
     u32 addr0 = 0, addr1 = 0, o0 = 0, o1 = 0;
     bool pair = false, fast01 = false;
-    if (!UNI || (sD & PK_DM_MEM)) {
+    {
         // operand pools: registers (w1:w0) and ext (q1:q0) = instruction bytes, m0|m1 and SP
         const u32 asrc = perm(w1, w0, m.AR) | perm(sp << 16, bytes, m.AE);
         addr0 = (asrc + (u32)sfield(D, PK_DB_AOFF, 2)) & 0xFFFFu;
@@ -439,7 +426,7 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     // ---------------- memory reads (m0 at addr0, m1 at addr1) ----------------
     const bool rd = bit(D, PK_DB_RD) != 0u, rd2 = bit(D, PK_DB_RD2) != 0u;
     u32 m16 = 0;
-    if (!UNI || (sD & (1u << PK_DB_RD))) {
+    {
         const bool rram = rd & fast01;  // addr1 == addr0 for 1-byte reads
         // staged ROM is 16 KB-aligned: inside one block addr1 is staged iff addr0 is, at index + ADIR
         const bool rrom = rd & rom_staged(s, addr0) & pair;
@@ -488,29 +475,24 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     u32 cin = 0, r = 0, cvx = 0, rs = 0, lres = 0;
     // carry-in of the adder, or the bit shifted in by the right-shift unit: bit CW of
     // (X | F << 16) ^ CI (F.C at bit 20, X's bits 7/0, bit 16 = 0 for the constants)
-    if (!UNI || (sU & ((1u << PK_US_ADD) | (1u << PK_US_RIGHT))))
-        cin = ((((X & 0xFFFFu) | (w1 & 0xFFFF0000u)) ^ m.CI) & m.CW) != 0u ? 1u : 0u;
+    cin = ((((X & 0xFFFFu) | (w1 & 0xFFFF0000u)) ^ m.CI) & m.CW) != 0u ? 1u : 0u;
     // adder: r = X + Y ^ YX + cin (YX = 0x1FFFF subtracts); X ^ Y ^ r = the carry (borrow) into
     // each bit.  Left rotates and shifts are X + X + (0 / F.C / bit 7): bit 8 is the carry out
-    if (!UNI || (sU & (1u << PK_US_ADD))) {
-        r = X + (Y ^ m.YX) + cin;
-        cvx = X ^ Y ^ r;
-    }
+    r = X + (Y ^ m.YX) + cin;
+    cvx = X ^ Y ^ r;
     // right-shift unit: RRC RRA RR SRA SRL ((X | in << 8 | X.0 << 9) >> 1: bit 8 = the bit
     // shifted out) and SWAP ((X | X << 8) >> 4)
-    if (!UNI || (sU & (1u << PK_US_RIGHT))) {
+    {
         const bool swap = bit(U, PK_US_SWAP) != 0u;
         rs = (X | (sel(swap, X, cin | ((X & 1u) << 1)) << 8)) >> sel(swap, 4u, 1u);
     }
     // logic: (X & Y) and/or (X ^ Y) (OR = both); loads are 0xFF AND Y
-    if (!UNI || (sU & (1u << PK_US_LOGIC)))
-        lres = ((X & Y) & (u32)sfield(U, PK_US_LAND, 1)) | ((X ^ Y) & (u32)sfield(U, PK_US_LXOR, 1));
+    lres = ((X & Y) & (u32)sfield(U, PK_US_LAND, 1)) | ((X ^ Y) & (u32)sfield(U, PK_US_LXOR, 1));
     u32 res8 = sel(bit(U, PK_US_LOGIC), lres, sel(right, rs, r)) & 0xFFu;
     // flags: F' = (F & FK) | ((Z | H | C | FC) & FM), H/C = carry bits 4/8 (12/16 for ADD HL) or
     // the right unit's shifted-out bit 8
     u32 nf = F;
-    const bool fchg = !UNI || uc_flags(sK, sU);
-    if (fchg) {
+    {
         const u32 cs = sel(right, rs, cvx) >> (bit(U, PK_US_HSH8) * 8u);
         const u32 fv = sel(res8 == 0u, 0x80u, 0u) | ((cs << 1) & 0x20u) | ((cs >> 4) & 0x10u) | K;
         nf = ((F & (K >> 8)) | (fv & (K >> 16))) & 0xFFu;
@@ -526,7 +508,7 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     // register writeback: val = res16 | F' << 16 | res8 << 24 through the per-op byte selectors
     // (res16: the adder, or HL +- 1 for (HL+)/(HL-); bytes 2-3 of either are not taken)
     const u32 u16 = sel(bit(U, PK_US_R16HL), w1 + (u32)sfield(U, PK_US_HLINC, 2), r);
-    if (!UNI || fchg || (sU & (1u << PK_US_REGW))) {
+    {
         const u32 val = perm(nf | (res8 << 8), u16, 0x05040100u);
         s.w0 = perm(val, w0, m.S0);
         s.w1 = perm(val, w1, m.S1);
@@ -535,14 +517,14 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     // ---------------- control transfer, SP, IME/HALT ----------------
     // JP/CALL/INT nn, JP HL, RET, RST: X | Y (one of them is 0); JR: pc + 2 + (Y = sext e)
     s.pc = pcn;
-    if (!UNI || (sU & (1u << PK_US_JUMP))) {
+    {
         const u32 tgt = (X + Y + (pcn & m.V)) & 0xFFFFu;
         const bool jump = bit(U, PK_US_JUMP) != 0u && taken != 0u;
         s.pc = sel(jump, tgt, pcn);
         ev |= sel(jump, PK_EV_JUMP, 0u);
     }
     x.cycles = ((D >> PK_DB_CYC) & 7u) * 4u + sel(taken != 0u, ((D >> PK_DB_XCYC) & 3u) * 4u, 0u);
-    if (!UNI || (sU & ((1u << PK_US_SPW) | (7u << PK_US_SPD)))) {
+    {
         const u32 sp2 = (sp + ((u32)sfield(U, PK_US_SPD, 3) & (0u - taken))) & 0xFFFFu;
         s.sp = sel(bit(U, PK_US_SPW), u16 & 0xFFFFu, sp2);
     }
@@ -563,10 +545,8 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     x.o1 = o1;
 }
 
-template <bool UNI>
-__device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc& m, u32 sD, const Ex& x, u32& ev) {
+__device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc& m, const Ex& x, u32& ev) {
     const PkStepArgs& A = *c.A;
-    if (UNI && !(sD & (1u << PK_DB_WR))) return;
     if (x.wram) {
         // VRAM / OAM change while rendered lines are pending: rasterise them first (rare)
         // (lines are pending only in the rendered frame: test that first, alone)
@@ -685,7 +665,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
     // software pipeline: the next instruction's bytes and microcode entry, loaded from LDS at the
     // end of the previous iteration (after its writes, so bank switches and HRAM code stores are
     // seen) while the timer/LCD work runs; pf = 0 -> fetch and decode at the top instead
-    u32 pf = 0, pbytes = 0, pdi = 0;   // pdi: the prefetched microcode index
+    u32 pf = 0, pbytes = 0;
     uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0, p2 = p0, p3 = p0;
 #ifdef PK_STAMP
     uint64_t st_acc[PK_NSTAMP] = {}, st_prev = __builtin_amdgcn_s_memtime(), st_iter = 0;
@@ -717,7 +697,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         }
 
         // ---------------- fetch + microcode entry (prefetched, or here when pf = 0) ----------------
-        u32 bytes = pbytes, cdi = pdi;
+        u32 bytes = pbytes;
         uint4 e0 = p0, e1 = p1, e2 = p2, e3 = p3;
         if (PK_RARE(!pf)) {
             PK_STAMP_AT(8);
@@ -757,7 +737,6 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             e1 = ucv[di * 4u + 1u];
             e2 = ucv[di * 4u + 2u];
             e3 = ucv[di * 4u + 3u];
-            cdi = di;
             PK_STAMP_AT(9);
         }
         icount += sel(exec, 1u, 0u);
@@ -766,15 +745,9 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         if (exec) PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, bytes & 0xFFu);
         const Mc m = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y, e2.z, e2.w, e3.x, e3.y, e3.z, e3.w};
         const u32 D = m.D;
-        // ---------------- execute: uniform (one microcode entry in every lane) or general ----------------
+        // ---------------- execute ----------------
         Ex x;
-        if (PK_WAVE_UNIFORM(cdi)) {
-            const u32 sD = __builtin_amdgcn_readfirstlane(m.D), sU = __builtin_amdgcn_readfirstlane(m.U),
-                      sK = __builtin_amdgcn_readfirstlane(m.K);
-            pk_exec<true, PRIO>(s, c, pc, bytes, m, sD, sU, sK, ev, x);
-        } else {
-            pk_exec<false, PRIO>(s, c, pc, bytes, m, m.D, m.U, m.K, ev, x);
-        }
+        pk_exec<PRIO>(s, c, pc, bytes, m, ev, x);
         u32 cycles = x.cycles;
         const bool wr = x.wr, wram = x.wram;
         // ---------------- fused secondary op (pk_ucode.h pk_u2_entry) ----------------
@@ -846,8 +819,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         }
 
         // ---------------- memory writes (wv0 at addr0, wv1 at addr1) ----------------
-        if (PK_WAVE_UNIFORM(cdi)) pk_write<true>(s, c, env, m, __builtin_amdgcn_readfirstlane(m.D), x, ev);
-        else pk_write<false>(s, c, env, m, m.D, x, ev);
+        pk_write(s, c, env, m, x, ev);
 
         // ---------------- prefetch the next instruction (LDS-staged ROM or the HRAM mirror) ----------------
         // wave priority (two waves per SIMD): from here through the next iteration's fetch, decode
@@ -875,7 +847,6 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             p1 = ucv[di * 4u + 1u];
             p2 = ucv[di * 4u + 2u];
             p3 = ucv[di * 4u + 3u];
-            pdi = di;
             pf = sel(fl | fh | fg, 1u, 0u);
         }
 

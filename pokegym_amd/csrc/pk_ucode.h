@@ -38,10 +38,8 @@ enum { PK_UE_D = 0, PK_UE_U, PK_UE_K, PK_UE_V, PK_UE_XR, PK_UE_XE, PK_UE_YR, PK_
 #define PK_US_FPOP 8      // F = m0 & 0xF0 (POP AF)
 #define PK_US_R16HL 9     // res16 = HL +- 1 (else adder)
 #define PK_US_SPW 10      // SP = res16
-#define PK_US_ADD 11      // the adder's result or carries are used (uniform iterations skip it otherwise)
 #define PK_US_LAND 12     // logic result includes X & Y (AND, OR)
 #define PK_US_LXOR 13     // logic result includes X ^ Y (XOR, OR)
-#define PK_US_REGW 14     // a register is written (writeback selectors other than the identity)
 #define PK_US_HLINC 22    // 2 bits signed HL increment for (HL+)/(HL-)
 #define PK_US_SPD 26      // 3 bits signed SP delta (PUSH/POP family), applied when the condition holds
 #define PK_UC_ENTRIES 515u
@@ -562,23 +560,6 @@ static inline void pk_store_uop(uint32_t* e, PkUop o, bool real) {
     if (!(real && ts == PK_T_NONE && !(o.d & (pk_fld(3, PK_DB_IME) | pk_fld(1, PK_DB_HALT) | pk_fld(1, PK_DB_CRASH) |
                                               pk_fld(1, PK_DB_DAA))) && (o.d & 3u) != 0u))
         e[PK_UE_D] |= pk_fld(1, PK_DB_NOFUSE);
-    {
-        // units a wave-uniform iteration may skip: the adder (result8 / res16 / H,C / Z not from it)
-        // and the register writeback
-        auto has = [](uint32_t sl, uint32_t v) {
-            for (int q = 0; q < 4; q++)
-                if (((sl >> (8 * q)) & 0xFFu) == v) return true;
-            return false;
-        };
-        const bool logic = (us & pk_fld(1, PK_US_LOGIC)) != 0u, rightu = (us & pk_fld(1, PK_US_RIGHT)) != 0u;
-        const bool r8used = has(o.s0, 7) || has(o.s1, 7) || (wr && !w16);
-        const bool r16used = has(o.s0, 4) || has(o.s0, 5) || has(o.s1, 4) || has(o.s1, 5) || (o.u & pk_fld(1, PK_UB_SPW));
-        const bool zf = (o.u & pk_fld(1, PK_UB_FZ)) != 0u, hcf = (o.u & pk_fld(1, PK_UB_FH)) != 0u || fcs != 0u;
-        const bool add = ((r8used || zf) && !logic && !rightu) || (r16used && !(o.u & pk_fld(1, PK_UB_R16HL)))
-                       || (hcf && !rightu);
-        if (add) us |= pk_fld(1, PK_US_ADD);
-        if (o.s0 != PK_S0_ID || o.s1 != PK_S1_ID) us |= pk_fld(1, PK_US_REGW);
-    }
     e[PK_UE_U] = us;
     e[PK_UE_K] = fconst | (fkeep << 8) | (fm << 16) | (cpu_keep << 24) | (cpu_set << 28);
     e[PK_UE_V] = jrm;

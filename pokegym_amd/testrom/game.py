@@ -58,6 +58,7 @@ wMathB equ $d472
 wMathR equ $d474
 wSound equ $d480
 wStepCount equ $d4a0
+wMapSeed equ $d4a1
 wSprState equ $d4c0
 
 section 0
@@ -163,6 +164,8 @@ start:
     ldh [hMenu], a
     ldh [hBGPortion], a
     ldh [hMoveTimer], a
+    ld a, $5a
+    ld [wMapSeed], a
     ld a, 1
     ld [wMoved], a
     ldh [hROMBank], a
@@ -332,6 +335,10 @@ handle_input:
     ldh [hMoveTimer], a
     ld hl, wStepCount
     inc [hl]
+    ; a door (floor metatile 3): warp into a new map, loaded with the LCD off
+    ld a, b
+    cp 3
+    jp z, map_warp
     ; grass: random encounter
     ld a, b
     cp 4
@@ -347,6 +354,59 @@ handle_input:
     ld [wBattleEnemyHP], a
     xor a
     ld [wBattleTurn], a
+    ret
+
+; pokered's map transition through a door (EnterMap -> LoadMapData): DisableLCD (wait for LY = 145,
+; LCD off), the new map's tileset graphics copied into VRAM and its blocks rebuilt in WRAM while the
+; LCD is off — several frames of bulk copies with no VBlank, the frames ending on the LCD-off clock
+; alone — then EnableLCD and a full map-view redraw
+map_warp:
+    ld a, [wMapSeed]
+    add a, 29
+    or 1
+    ld [wMapSeed], a
+.wly:
+    ldh a, [$44]
+    cp 145
+    jr nz, .wly
+    ldh a, [rLCDC]
+    and $7f
+    ldh [rLCDC], a
+    ; tileset graphics: 2 KiB of bank-0 bytes into tiles 128-255 ($8800-$8fff)
+    ld hl, $0100
+    ld de, $8800
+    ld bc, $0800
+.gfx:
+    ld a, [hl+]
+    ld [de], a
+    inc de
+    dec bc
+    ld a, b
+    or c
+    jr nz, .gfx
+    ; map blocks: the 64x64 metatile map from the new seed (the boot-time LFSR)
+    ld hl, wMap
+    ld bc, $1000
+    ld a, [wMapSeed]
+    ld e, a
+.blk:
+    ld a, e
+    add a, a
+    jr nc, .nox
+    xor $1d
+.nox:
+    ld e, a
+    and $07
+    ld [hl+], a
+    dec bc
+    ld a, b
+    or c
+    jr nz, .blk
+    ldh a, [rLCDC]
+    or $80
+    ldh [rLCDC], a
+    ld a, 1
+    ld [wMoved], a
     ret
 
 update_npcs:

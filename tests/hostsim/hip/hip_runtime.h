@@ -105,10 +105,6 @@ extern "C" void pk_sim_trace(uint32_t env, uint32_t pc, uint32_t w0, uint32_t w1
 // per-iteration event bits (iteration statistics for kernel design; see pk_kernels.hip PK_EV_*)
 extern "C" void pk_sim_iter(uint32_t env, uint32_t ev);
 #define PK_ITER(env, ev) pk_sim_iter(env, ev)
-// wave-uniform iterations: one lane per thread here, so "every lane holds the same entry" is true;
-// pk_sim_set_uniform(0) runs the general (all-units) path instead, so tests cover both
-extern "C" int pk_sim_uniform(void);
-#define PK_WAVE_UNIFORM(v) ((void)(v), pk_sim_uniform() != 0)
 // per-iteration microcode index (design statistics: opcode uniformity of a wave)
 extern "C" void pk_sim_iter_op(uint32_t env, uint32_t di);
 #define PK_ITER_OP(env, di) pk_sim_iter_op(env, di)

@@ -78,11 +78,6 @@ extern "C" uint64_t pk_sim_trace_get(uint32_t* out, uint64_t cap) {
     return n;
 }
 
-// ---- which K1 execute path runs (PK_WAVE_UNIFORM) ----
-static int g_uniform = 1;
-extern "C" void pk_sim_set_uniform(int on) { g_uniform = on; }
-extern "C" int pk_sim_uniform(void) { return g_uniform; }
-
 // ---- per-iteration event recording (PK_ITER) ----
 static std::vector<std::vector<uint32_t>> g_iter;
 static std::vector<std::vector<uint32_t>> g_iter_op;

@@ -157,3 +157,38 @@ def test_hram_code_parity(shape, monkeypatch):
     gpu, ref = _run_both(hram_code_rom(), None, n, 4, 31)
     bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
     assert not bad, bad[:4]
+
+
+def warp_actions(n, seed=5):
+    """Actions (6, n) from the warp fixture's state: columns 0..n/2-1 the recorded actions (they
+    walk through a door at step 2: pkbench's map load with the LCD off for ~5 frames), the rest
+    seeded random presses."""
+    d = np.load(os.path.join(GOLD, "warp_state.npz"))
+    acts = np.random.default_rng(seed).integers(0, 9, size=(len(d["actions"]), n), dtype=np.uint8)
+    acts[:, :n // 2] = d["actions"][:, None]
+    return d["state"].tobytes(), acts
+
+
+@pytest.mark.parametrize("shape", [("", ""), ("16", "512"), ("32", "512")])
+def test_map_load_warp_parity(shape, monkeypatch):
+    """pkbench's door warp (DisableLCD, 2 KiB of VRAM and 4 KiB of WRAM copied over ~5 LCD-off
+    frames, EnableLCD) from the fixture state, in lockstep and beside diverging envs, at the small
+    launch shape and the benchmarked 512-thread shapes; whole v9 state vs the oracle."""
+    import torch
+    from pokegym_amd.emulator import BatchedEmulator
+    from pokegym_amd.testrom.game import game_rom
+    lanes, block = shape
+    if lanes:
+        monkeypatch.setenv("PK_WAVE_LANES", lanes)
+        monkeypatch.setenv("PK_K1_BLOCK", block)
+    rom, n = game_rom(), 128
+    state, acts = warp_actions(n)
+    emu = BatchedEmulator(rom, n, state=state, render=True)
+    for t in range(len(acts)):
+        emu.step(torch.from_numpy(acts[t]).to(emu.device))
+    torch.cuda.synchronize()
+    gpu = [emu.snapshot(e) for e in range(n)]
+    emu.close()
+    ref, _ = oracle.batch_run(rom, state, acts, want_screens=False)
+    bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
+    assert not bad, bad[:4]

@@ -51,16 +51,23 @@ def test_hostsim_hram_code():
     assert check(hram_code_rom(), 8, 3, 5) == []
 
 
-@pytest.mark.parametrize("seed", [0, 3, 21, 58])
-def test_hostsim_general_execute_path(seed):
-    """The host simulation runs one lane per thread, so by default every iteration takes K1's
-    wave-uniform execute path (pk_exec<true>: scalar branches around unused units); this runs the
-    general all-units path (pk_exec<false>, what divergent waves execute) against the oracle."""
-    from tests.hostsim import sim
-    L = sim.lib()
-    L.pk_sim_set_uniform(0)
-    try:
-        assert check(fuzz_rom(seed), 8, 3, seed) == []
-        assert check(game_rom(), 4, 4, seed) == []
-    finally:
-        L.pk_sim_set_uniform(1)
+def test_hostsim_map_load_warp():
+    """pkbench's door warp (LCD off for ~5 frames of bulk VRAM/WRAM copies) from the fixture state
+    (tests/golden/warp_state.npz, tools/make_golden_warp.py)."""
+    import numpy as np
+    from oracle import oracle
+    from tests.hostsim.sim import SimEmulator
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "warp_state.npz"))
+    state = d["state"].tobytes()
+    n = 4
+    acts = np.random.default_rng(5).integers(0, 9, size=(len(d["actions"]), n), dtype=np.uint8)
+    acts[:, :2] = d["actions"][:, None]
+    rom = game_rom()
+    emu = SimEmulator(rom, n, state=state)
+    for t in range(len(acts)):
+        emu.step(acts[t])
+    ref, _ = oracle.batch_run(rom, state, acts, want_screens=False)
+    bad = [e for e in range(n) if emu.snapshot(e) != ref[e].tobytes()]
+    assert not bad, bad
+    # the recorded envs did warp: wMapSeed (0xD4A1, v9 WRAM at 101285) moved on from its boot value
+    assert ref[0][101285 + 0x14A1] != 0x5A

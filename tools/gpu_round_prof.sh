@@ -24,6 +24,8 @@ for spec in "$@"; do
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $D/write -o write --output-format csv -- \
       python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline $args > $D/write_bench.json 2> $D/write.err && \
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d $D/valu -o valu --output-format csv -- \
-      python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline $args > $D/valu_bench.json 2> $D/valu.err || { rc=$?; break; }
+      python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline $args > $D/valu_bench.json 2> $D/valu.err && \
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM -d $D/issue -o issue --output-format csv -- \
+      python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline $args > $D/issue_bench.json 2> $D/issue.err || { rc=$?; break; }
 done
 echo "exit=$rc" > $OUT/exit.txt

@@ -53,6 +53,21 @@ def main():
             if "pk_step_kernel" in row["Name"]:
                 k1.append(float(row["AverageNs"]) / 1e6)
     bench = json.loads(open(os.path.join(D, "stats_bench.json")).read().strip().splitlines()[-1])
+    # issue: ISA instructions a wave issues per emulated SM83 instruction of one of its envs
+    # (SQ_INSTS_* / SQ_WAVES / the instructions one env executes in the launch)
+    issue = None
+    if os.path.isdir(os.path.join(D, "issue")):
+        q = per_dispatch(os.path.join(D, "issue"), "pk_step_kernel")
+        ib = json.loads(open(os.path.join(D, "issue_bench.json")).read().strip().splitlines()[-1])
+        ipe = ib["instr_per_env_step"]
+        waves = mean(q, "SQ_WAVES")
+        per = {k.replace("SQ_INSTS_", "").lower(): round(mean(q, k) / waves / ipe, 1)
+               for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_BRANCH", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD",
+                         "SQ_INSTS_VMEM_WR", "SQ_INSTS_SMEM")}
+        per["total"] = round(sum(per.values()), 1)
+        issue = {"isa_per_emulated_instr": per, "instr_per_env_step": ipe,
+                 "method": "rocprofv3 --pmc SQ_INSTS_* of the K1 launches after the first: wave instructions / "
+                           "SQ_WAVES / emulated instructions per env (the device's instruction counter)"}
     out = {
         "workload": bench["config"]["workload"],
         "envs_per_gpu": bench["config"]["envs_per_gpu"],
@@ -68,8 +83,10 @@ def main():
         "valu_busy_formula": "100*sum(SQ_ACTIVE_INST_VALU)/CU_NUM/max(GRBM_GUI_ACTIVE) (rocprofv3 VALUBusy, gfx94x form)",
         "valu_utilization_pct": round(util, 2),
         "valu_utilization_formula": "100*sum(SQ_THREAD_CYCLES_VALU)/(sum(SQ_ACTIVE_INST_VALU)*64): active lanes per VALU "
-                                    "instruction (K1 runs 32 envs in each 64-lane wave at 65,536 envs, so <= 50 %)",
+                                    "instruction, out of 64 (a wave carries wave_lanes envs: 16, 32 or 64 by launch "
+                                    "size, so at most wave_lanes/64)",
         "wait_any_pct": round(wait, 2),
+        "issue": issue,
         "waves_per_launch": mean(v, "SQ_WAVES"),
         "k1_avg_ms_rocprof_stats": round(k1[0], 3) if k1 else None,
         "bench_under_rocprof": {"value": bench["value"], "k1_ms": bench["roofline"]["k1_ms"],
