@@ -745,6 +745,9 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         if (exec) PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, bytes & 0xFFu);
         const Mc m = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y, e2.z, e2.w, e3.x, e3.y, e3.z, e3.w};
         const u32 D = m.D;
+        // the successor's secondary-op entry (read now: its LDS latency overlaps the execute stage)
+        const u32 nxt = bytes >> (8u * (D & 3u));
+        const uint4 u2 = ucv2[(nxt & 0xFFu) | (D & (1u << PK_DB_NOFUSE))];
         // ---------------- execute ----------------
         Ex x;
         pk_exec<PRIO>(s, c, pc, bytes, m, ev, x);
@@ -761,8 +764,6 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         // fetched bytes stay valid), both instructions within the 3 bytes every fetch path provides
         // (ROM code has 4), and none of them an IO register (DIV and a folded STAT change with the clock).
         {
-            const u32 nxt = bytes >> (8u * (D & 3u));
-            const uint4 u2 = ucv2[(nxt & 0xFFu) | (D & (1u << PK_DB_NOFUSE))];
             const u32 len2 = u2.y & 3u;
             // both instructions within the fetched bytes: 4 for ROM code, 3 for code in RAM
             const bool lenok = (D & 3u) + len2 + sel(pc >= 0x8000u, 1u, 0u) <= 4u;
@@ -851,148 +852,159 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         }
 
         // ---------------- HALT fast-forward, timer, LCD (pyboy mb.tick) ----------------
-        const u32 tac = s.tim0 >> 24;
-        // HALT skip-ahead: a halted CPU that nothing can wake before VBlank (no pending or queued
-        // interrupt, timer off, STAT HBlank/OAM/LYC interrupts off, frame not rendered) would spend
-        // one loop iteration per LCD mode event (3 per scanline) fast-forwarding to it.  Jump to
-        // the state right after line 143's mode-0 event in one step instead (exactly the state those
-        // iterations would reach: LY, STAT mode and coincidence bit, clock, DIV, watchdog budget),
-        // so the VBlank event itself is processed below as usual.
-        // Both halted-CPU blocks sit behind one `if`: a wave has a halted lane in only a few % of
-        // its iterations, so the others skip their ~50 instructions.
-        PK_STAMP_AT(5);
-        if (PK_RARE(s.cpu & CPU_HALT)) {
-            // a halted CPU fast-forwards to the next LCD event and notices pending interrupts only
-            // there, so folded events are observable here: restore the exact event state first
-            lcd_unfold(s);
-            const u32 cpu = s.cpu, stat = bfe8(s.lcd0, 8), ly = bfe8(s.lcd0, 16), nm = (s.lcd2 >> 24) & 3u;
-            const bool cand = !(cpu & CPU_QUEUED) && ((cpu >> 8) & (cpu >> 16) & 0x1Fu) == 0u
-                           && (s.lcd0 & 0x80u) && (stat & 0x68u) == 0u && !(tac & 4u) && ly < 143u && nm != 1u && s.clock <= s.target;
-            const u32 lines = 143u - ly;
-            const u32 vbl = sel(nm == 2u, s.target + 456u * lines, s.target - sel(nm == 3u, 80u, 250u) + 456u * (lines + 1u));
-            const u32 nev = sel(nm == 3u, 2u, sel(nm == 0u, 1u, 0u)) + 3u * lines + 1u;  // iterations up to VBlank
-            const u32 tnew = vbl - 206u;                                                  // line 143 mode-0 event
-            if (cand && (int)((vbl - s.clock) + nev) <= slack) {
-                if (s.render) {
-                    // rendered frame: the skipped mode-0 events would latch every remaining line with
-                    // the (unchanging, the CPU is halted) scroll/window/palette registers — latch
-                    // them here, advancing the window line counter as the per-event latch does
-                    const u32 lcdc = s.lcd0 & 0xFFu, wy = bfe8(s.lcd1, 16), wx = bfe8(s.lcd1, 24);
-                    const u32 l0 = lcdc | (bfe8(s.lcd1, 8) << 8) | (bfe8(s.lcd1, 0) << 16) | (wx << 24);
-                    const u32 l1 = wy | ((s.lcd2 & 0xFFFFFFu) << 8);
-                    const bool wline = (lcdc & 0x20u) && (int)wx - 7 < (int)PK_COLS;
-                    int lw = (int)bfe8(s.misc, 16) - 1;
-                    const u32 y0 = sel(nm == 2u, ly + 1u, ly);   // nm 2: this line's mode-0 event has passed
-                    for (u32 y = y0; y < PK_ROWS; y++) {
-                        if (wline && wy <= y) lw += 1;
-                        const u32 idx = (c.gid * PK_ROWS + y) * PK_LANES + c.lane;
-                        A.lat[idx] = l0;
-                        A.lat[A.lat_stride + idx] = l1;
-                        A.lat[2u * A.lat_stride + idx] = (u32)(lw + 1) | 0x100u;
+        // Common case: a running CPU whose cycles reach neither the next LCD event (nor, LCD off,
+        // the frame length), with the timer off and the watchdog budget left — then the whole stage
+        // is DIV, clock and watchdog bookkeeping (no interrupt, no latch, no frame end).
+        const u32 clk2 = s.clock + cycles;
+        const u32 lim = sel(s.lcd0 & 0x80u, s.target, FRAME_CYCLES);
+        if (PK_RARE((s.cpu & CPU_HALT) | (s.tim0 & (4u << 24)) | (clk2 >= lim) | ((int)(cycles + 1u) > slack))) {
+            const u32 tac = s.tim0 >> 24;
+            // HALT skip-ahead: a halted CPU that nothing can wake before VBlank (no pending or queued
+            // interrupt, timer off, STAT HBlank/OAM/LYC interrupts off, frame not rendered) would spend
+            // one loop iteration per LCD mode event (3 per scanline) fast-forwarding to it.  Jump to
+            // the state right after line 143's mode-0 event in one step instead (exactly the state those
+            // iterations would reach: LY, STAT mode and coincidence bit, clock, DIV, watchdog budget),
+            // so the VBlank event itself is processed below as usual.
+            // Both halted-CPU blocks sit behind one `if`: a wave has a halted lane in only a few % of
+            // its iterations, so the others skip their ~50 instructions.
+            PK_STAMP_AT(5);
+            if (PK_RARE(s.cpu & CPU_HALT)) {
+                // a halted CPU fast-forwards to the next LCD event and notices pending interrupts only
+                // there, so folded events are observable here: restore the exact event state first
+                lcd_unfold(s);
+                const u32 cpu = s.cpu, stat = bfe8(s.lcd0, 8), ly = bfe8(s.lcd0, 16), nm = (s.lcd2 >> 24) & 3u;
+                const bool cand = !(cpu & CPU_QUEUED) && ((cpu >> 8) & (cpu >> 16) & 0x1Fu) == 0u
+                               && (s.lcd0 & 0x80u) && (stat & 0x68u) == 0u && !(tac & 4u) && ly < 143u && nm != 1u && s.clock <= s.target;
+                const u32 lines = 143u - ly;
+                const u32 vbl = sel(nm == 2u, s.target + 456u * lines, s.target - sel(nm == 3u, 80u, 250u) + 456u * (lines + 1u));
+                const u32 nev = sel(nm == 3u, 2u, sel(nm == 0u, 1u, 0u)) + 3u * lines + 1u;  // iterations up to VBlank
+                const u32 tnew = vbl - 206u;                                                  // line 143 mode-0 event
+                if (cand && (int)((vbl - s.clock) + nev) <= slack) {
+                    if (s.render) {
+                        // rendered frame: the skipped mode-0 events would latch every remaining line with
+                        // the (unchanging, the CPU is halted) scroll/window/palette registers — latch
+                        // them here, advancing the window line counter as the per-event latch does
+                        const u32 lcdc = s.lcd0 & 0xFFu, wy = bfe8(s.lcd1, 16), wx = bfe8(s.lcd1, 24);
+                        const u32 l0 = lcdc | (bfe8(s.lcd1, 8) << 8) | (bfe8(s.lcd1, 0) << 16) | (wx << 24);
+                        const u32 l1 = wy | ((s.lcd2 & 0xFFFFFFu) << 8);
+                        const bool wline = (lcdc & 0x20u) && (int)wx - 7 < (int)PK_COLS;
+                        int lw = (int)bfe8(s.misc, 16) - 1;
+                        const u32 y0 = sel(nm == 2u, ly + 1u, ly);   // nm 2: this line's mode-0 event has passed
+                        for (u32 y = y0; y < PK_ROWS; y++) {
+                            if (wline && wy <= y) lw += 1;
+                            const u32 idx = (c.gid * PK_ROWS + y) * PK_LANES + c.lane;
+                            A.lat[idx] = l0;
+                            A.lat[A.lat_stride + idx] = l1;
+                            A.lat[2u * A.lat_stride + idx] = (u32)(lw + 1) | 0x100u;
+                        }
+                        s.misc = setb8(s.misc, 16, 0u);              // reset after line 143
+                        s.npend += PK_ROWS - y0;
                     }
-                    s.misc = setb8(s.misc, 16, 0u);              // reset after line 143
-                    s.npend += PK_ROWS - y0;
+                    const u32 skipped = tnew - s.clock;
+                    s.divacc = (s.divacc + skipped) & 0xFFFFu;
+                    slack -= (int)(skipped + (nev - 1u));
+                    s.clock = tnew;
+                    s.target = vbl;
+                    const u32 st2 = (stat & 0xF8u) | sel((s.lcd0 >> 24) == 143u, 4u, 0u);
+                    s.lcd0 = (s.lcd0 & 0xFF0000FFu) | (st2 << 8) | (143u << 16);
+                    s.lcd2 = (s.lcd2 & 0x00FFFFFFu) | (1u << 24);
                 }
-                const u32 skipped = tnew - s.clock;
-                s.divacc = (s.divacc + skipped) & 0xFFFFu;
-                slack -= (int)(skipped + (nev - 1u));
-                s.clock = tnew;
-                s.target = vbl;
-                const u32 st2 = (stat & 0xF8u) | sel((s.lcd0 >> 24) == 143u, 4u, 0u);
-                s.lcd0 = (s.lcd0 & 0xFF0000FFu) | (st2 << 8) | (143u << 16);
-                s.lcd2 = (s.lcd2 & 0x00FFFFFFu) | (1u << 24);
+                const u32 dsh = timer_shift(tac);
+                const int tb = (int)sel(tac & 4u, ((0x100u - bfe8(s.tim0, 8)) << dsh) - s.timac, 1u << 16);
+                const int ta = (int)s.target - (int)s.clock;
+                const int mm = ta < tb ? ta : tb;
+                cycles = (u32)(mm < 0 ? 0 : mm);
+                PK_STAMP_AT(6);
             }
-            const u32 dsh = timer_shift(tac);
-            const int tb = (int)sel(tac & 4u, ((0x100u - bfe8(s.tim0, 8)) << dsh) - s.timac, 1u << 16);
-            const int ta = (int)s.target - (int)s.clock;
-            const int mm = ta < tb ? ta : tb;
-            cycles = (u32)(mm < 0 ? 0 : mm);
-            PK_STAMP_AT(6);
-        }
-        u32 irq = 0;
-        s.divacc = (s.divacc + cycles) & 0xFFFFu;
-        if (PK_RARE(tac & 4u)) {  // TAC enabled (timer.py Timer.tick)
-            const u32 dsh = timer_shift(tac);
-            u32 timac = s.timac + cycles;
-            u32 tima = bfe8(s.tim0, 8);
-            const u32 mul = timac >> dsh;
-            timac -= mul << dsh;
-            tima += mul;
-            const bool ovf = tima > 0xFFu;
-            tima = sel(ovf, (tima - 0x100u + bfe8(s.tim0, 16)) & 0xFFu, tima);
-            irq |= sel(ovf, 4u, 0u);
-            ev |= sel(ovf, PK_EV_TIMER, 0u);
-            s.tim0 = setb8(s.tim0, 8, tima);
-            s.timac = timac;
-        }
-        s.clock += cycles;
-        const u32 lcdc = s.lcd0 & 0xFFu;
-        const bool lcdev = (lcdc & 0x80u) && s.clock >= s.target;
-        if (lcdev) {  // lcd.tick mode transition
-            const u32 nm = (s.lcd2 >> 24) & 3u;
-            u32 stat = bfe8(s.lcd0, 8), ly = sel(s.lcd2 & PK_LCD_FFOLD, sel(nm == 1u, 143u, 153u), bfe8(s.lcd0, 16));
-            const u32 lyc = s.lcd0 >> 24;
-            const bool changed = (stat & 3u) != nm;
-            stat = (stat & 0xFCu) | nm;
-            irq |= sel(changed && nm != 3u && ((stat >> (nm + 3u)) & 1u), 2u, 0u);
-            const bool m2 = nm == 2u, m3 = nm == 3u, m0 = nm == 0u, m1 = nm == 1u;
-            const bool wrap = m2 && ly == 153u;  // clock, target < 2 frames: one subtraction
-            s.clock -= sel(wrap && s.clock >= FRAME_CYCLES, FRAME_CYCLES, 0u);
-            s.target -= sel(wrap && s.target >= FRAME_CYCLES, FRAME_CYCLES, 0u);
-            ly = sel(wrap, 0u, sel(m2 || m1, ly + 1u, ly));
-            const bool fold = m2 && (stat & 0x38u) == 0u && !s.render;  // see lcd_unfold
-            // folded runs: the rest of the visible frame, or VBlank lines 145-153 (from the VBlank event)
-            const bool vfold = m1 && ly == 144u && (stat & 0x40u) == 0u;
-            const bool ffold = (fold && (stat & 0x40u) == 0u && ly < 143u) || vfold;
-            s.target += sel(ffold, 456u * sel(vfold, 10u, 144u - ly), sel(fold, 456u, sel(m2, 80u, sel(m3, 170u, sel(m0, 206u, 456u)))));
-            const bool eq = lyc == ly, upd = m2 || m1;
-            stat = sel(upd, sel(eq, stat | 4u, stat & 0xFBu), stat);
-            irq |= sel(upd && eq && (stat & 0x40u), 2u, 0u);
-            const u32 nnext = sel(m2 && !fold, 3u, sel(m3, 0u, sel(m0 || fold, sel(ly < 143u && !ffold, 2u, 1u),
-                                                                   sel(ly == 153u || vfold, 2u, 1u))));
-            const bool vbl = m1 && ly == 144u;
-            irq |= sel(vbl, 1u, 0u);
-            s.frame_done |= sel(vbl, 1u, 0u);
-            s.lcd0 = (s.lcd0 & 0xFF0000FFu) | (stat << 8) | (ly << 16);
-            s.lcd2 = (s.lcd2 & 0x00FFFFFFu) | (nnext << 24) | sel(ffold, PK_LCD_FFOLD, sel(fold, PK_LCD_FOLD, 0u));
-        }
-        ev |= sel(lcdev, PK_EV_LCD, 0u);
-        {
-            // latch this scanline's registers at its mode-0 event in the rendered frame; K2 (or
-            // flush_lines) rasterises it later
-            const u32 ly = bfe8(s.lcd0, 16);
-            if (PK_RARE(lcdev && s.render && (s.lcd0 & 0x300u) == 0u && ly < PK_ROWS)) {
-                const u32 wy = bfe8(s.lcd1, 16), wx = bfe8(s.lcd1, 24);
-                int lw = (int)bfe8(s.misc, 16) - 1;
-                if ((lcdc & 0x20u) && wy <= ly && (int)wx - 7 < (int)PK_COLS) lw += 1;
-                const u32 idx = (c.gid * PK_ROWS + ly) * PK_LANES + c.lane;
-                A.lat[idx] = lcdc | (bfe8(s.lcd1, 8) << 8) | (bfe8(s.lcd1, 0) << 16) | (wx << 24);
-                A.lat[A.lat_stride + idx] = wy | ((s.lcd2 & 0xFFFFFFu) << 8);
-                A.lat[2u * A.lat_stride + idx] = (u32)(lw + 1) | 0x100u;
-                if (ly == PK_ROWS - 1u) lw = -1;
-                s.misc = setb8(s.misc, 16, (u32)(lw + 1));
-                s.npend += 1u;
+            u32 irq = 0;
+            s.divacc = (s.divacc + cycles) & 0xFFFFu;
+            if (PK_RARE(tac & 4u)) {  // TAC enabled (timer.py Timer.tick)
+                const u32 dsh = timer_shift(tac);
+                u32 timac = s.timac + cycles;
+                u32 tima = bfe8(s.tim0, 8);
+                const u32 mul = timac >> dsh;
+                timac -= mul << dsh;
+                tima += mul;
+                const bool ovf = tima > 0xFFu;
+                tima = sel(ovf, (tima - 0x100u + bfe8(s.tim0, 16)) & 0xFFu, tima);
+                irq |= sel(ovf, 4u, 0u);
+                ev |= sel(ovf, PK_EV_TIMER, 0u);
+                s.tim0 = setb8(s.tim0, 8, tima);
+                s.timac = timac;
             }
+            s.clock += cycles;
+            const u32 lcdc = s.lcd0 & 0xFFu;
+            const bool lcdev = (lcdc & 0x80u) && s.clock >= s.target;
+            if (lcdev) {  // lcd.tick mode transition
+                const u32 nm = (s.lcd2 >> 24) & 3u;
+                u32 stat = bfe8(s.lcd0, 8), ly = sel(s.lcd2 & PK_LCD_FFOLD, sel(nm == 1u, 143u, 153u), bfe8(s.lcd0, 16));
+                const u32 lyc = s.lcd0 >> 24;
+                const bool changed = (stat & 3u) != nm;
+                stat = (stat & 0xFCu) | nm;
+                irq |= sel(changed && nm != 3u && ((stat >> (nm + 3u)) & 1u), 2u, 0u);
+                const bool m2 = nm == 2u, m3 = nm == 3u, m0 = nm == 0u, m1 = nm == 1u;
+                const bool wrap = m2 && ly == 153u;  // clock, target < 2 frames: one subtraction
+                s.clock -= sel(wrap && s.clock >= FRAME_CYCLES, FRAME_CYCLES, 0u);
+                s.target -= sel(wrap && s.target >= FRAME_CYCLES, FRAME_CYCLES, 0u);
+                ly = sel(wrap, 0u, sel(m2 || m1, ly + 1u, ly));
+                const bool fold = m2 && (stat & 0x38u) == 0u && !s.render;  // see lcd_unfold
+                // folded runs: the rest of the visible frame, or VBlank lines 145-153 (from the VBlank event)
+                const bool vfold = m1 && ly == 144u && (stat & 0x40u) == 0u;
+                const bool ffold = (fold && (stat & 0x40u) == 0u && ly < 143u) || vfold;
+                s.target += sel(ffold, 456u * sel(vfold, 10u, 144u - ly), sel(fold, 456u, sel(m2, 80u, sel(m3, 170u, sel(m0, 206u, 456u)))));
+                const bool eq = lyc == ly, upd = m2 || m1;
+                stat = sel(upd, sel(eq, stat | 4u, stat & 0xFBu), stat);
+                irq |= sel(upd && eq && (stat & 0x40u), 2u, 0u);
+                const u32 nnext = sel(m2 && !fold, 3u, sel(m3, 0u, sel(m0 || fold, sel(ly < 143u && !ffold, 2u, 1u),
+                                                                       sel(ly == 153u || vfold, 2u, 1u))));
+                const bool vbl = m1 && ly == 144u;
+                irq |= sel(vbl, 1u, 0u);
+                s.frame_done |= sel(vbl, 1u, 0u);
+                s.lcd0 = (s.lcd0 & 0xFF0000FFu) | (stat << 8) | (ly << 16);
+                s.lcd2 = (s.lcd2 & 0x00FFFFFFu) | (nnext << 24) | sel(ffold, PK_LCD_FFOLD, sel(fold, PK_LCD_FOLD, 0u));
+            }
+            ev |= sel(lcdev, PK_EV_LCD, 0u);
+            {
+                // latch this scanline's registers at its mode-0 event in the rendered frame; K2 (or
+                // flush_lines) rasterises it later
+                const u32 ly = bfe8(s.lcd0, 16);
+                if (PK_RARE(lcdev && s.render && (s.lcd0 & 0x300u) == 0u && ly < PK_ROWS)) {
+                    const u32 wy = bfe8(s.lcd1, 16), wx = bfe8(s.lcd1, 24);
+                    int lw = (int)bfe8(s.misc, 16) - 1;
+                    if ((lcdc & 0x20u) && wy <= ly && (int)wx - 7 < (int)PK_COLS) lw += 1;
+                    const u32 idx = (c.gid * PK_ROWS + ly) * PK_LANES + c.lane;
+                    A.lat[idx] = lcdc | (bfe8(s.lcd1, 8) << 8) | (bfe8(s.lcd1, 0) << 16) | (wx << 24);
+                    A.lat[A.lat_stride + idx] = wy | ((s.lcd2 & 0xFFFFFFu) << 8);
+                    A.lat[2u * A.lat_stride + idx] = (u32)(lw + 1) | 0x100u;
+                    if (ly == PK_ROWS - 1u) lw = -1;
+                    s.misc = setb8(s.misc, 16, (u32)(lw + 1));
+                    s.npend += 1u;
+                }
+            }
+            if (PK_RARE(!(lcdc & 0x80u) && s.clock >= FRAME_CYCLES)) {  // LCD off: the frame ends on the clock alone
+                s.frame_done = 1u;
+                s.clock %= FRAME_CYCLES;
+                s.blank |= s.render;
+            }
+            s.cpu |= irq << 16;
+            PK_STAMP_AT(7);
+            slack -= (int)(cycles + 1u);
+            ev |= sel(s.frame_done != 0u || slack < 0, PK_EV_FRAME, 0u);
+            if (PK_RARE((s.frame_done != 0u) | (slack < 0))) {  // frame end or watchdog
+                s.frame_done = 0;
+                slack = (int)(16u * FRAME_CYCLES);
+                frame += 1u;
+                if (frame == A.release_frame && btn != 0xFFu) key_event(s, btn, false);
+                s.render = (A.render_last && frame + 1u == A.frames) ? 1u : 0u;
+            }
+        } else {
+            s.divacc = (s.divacc + cycles) & 0xFFFFu;
+            s.clock = clk2;
+            slack -= (int)(cycles + 1u);
         }
-        if (PK_RARE(!(lcdc & 0x80u) && s.clock >= FRAME_CYCLES)) {  // LCD off: the frame ends on the clock alone
-            s.frame_done = 1u;
-            s.clock %= FRAME_CYCLES;
-            s.blank |= s.render;
-        }
-        s.cpu |= irq << 16;
-        PK_STAMP_AT(7);
-        slack -= (int)(cycles + 1u);
-        ev |= sel(s.frame_done != 0u || slack < 0, PK_EV_FRAME, 0u);
         PK_ITER(env, ev);
         PK_ITER_OP(env, sel(exec, sel((bytes & 0xFFu) == 0xCBu, 256u + ((bytes >> 8) & 0xFFu), bytes & 0xFFu),
                             sel(dispatch, PK_UC_INT, sel(doint, PK_UC_NOP0, PK_UC_IDLE))));
-        if (PK_RARE((s.frame_done != 0u) | (slack < 0))) {  // frame end or watchdog
-            s.frame_done = 0;
-            slack = (int)(16u * FRAME_CYCLES);
-            frame += 1u;
-            if (frame == A.release_frame && btn != 0xFFu) key_event(s, btn, false);
-            s.render = (A.render_last && frame + 1u == A.frames) ? 1u : 0u;
-        }
     }
 
 #ifdef PK_STAMP

@@ -166,6 +166,7 @@ start:
     ldh [hMoveTimer], a
     ld a, $5a
     ld [wMapSeed], a
+    call set_party
     ld a, 1
     ld [wMoved], a
     ldh [hROMBank], a
@@ -365,6 +366,14 @@ map_warp:
     add a, 29
     or 1
     ld [wMapSeed], a
+    ; DisableLCD: VBlank interrupt off while waiting for LY = 145 (the handler runs longer than a
+    ; scanline, so with it enabled the poll would never see line 145)
+    xor a
+    ldh [$0f], a
+    ldh a, [$ff]
+    push af
+    res 0, a
+    ldh [$ff], a
 .wly:
     ldh a, [$44]
     cp 145
@@ -402,11 +411,34 @@ map_warp:
     ld a, b
     or c
     jr nz, .blk
+    call set_party
     ldh a, [rLCDC]
     or $80
     ldh [rLCDC], a
+    xor a
+    ldh [$0f], a
+    pop af
+    ldh [$ff], a
     ld a, 1
     ld [wMoved], a
+    ret
+
+; the party: one level-5 Bulbasaur with 20/20 HP at pokered's wPartyCount/wPartyMons addresses (the
+; reference's save states always hold a party — an empty one makes its info step raise,
+; environment.py:1672).  They lie inside the 4 KiB map blocks, so every map (re)build rewrites them
+set_party:
+    ld a, 1
+    ld [$d163], a
+    ld a, $99
+    ld [$d164], a
+    ld [$d16b], a
+    ld a, $ff
+    ld [$d165], a
+    ld a, 5
+    ld [$d18c], a
+    ld a, 20
+    ld [$d16d], a
+    ld [$d18e], a
     ret
 
 update_npcs:

@@ -6,14 +6,19 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
+from tests.pkbench_state import pkbench_power_on  # noqa: E402
+
+
 
 @pytest.mark.gpu
 def test_environment_reset_step_shapes(tmp_path):
     from pokegym_amd.env import Environment
-    from pokegym_amd.testrom.game import game_rom
+    rom_bytes, state = pkbench_power_on()
     rom = tmp_path / "pkbench.gb"
-    rom.write_bytes(game_rom())
-    env = Environment(rom_path=str(rom), max_episode_steps=3)
+    rom.write_bytes(rom_bytes)
+    st = tmp_path / "pkbench.state"
+    st.write_bytes(state)
+    env = Environment(rom_path=str(rom), state_path=str(st), max_episode_steps=3)
     obs, info = env.reset()
     assert obs.shape == (72, 80, 4) and obs.dtype == np.uint8 and info == {}
     for t in range(3):
@@ -29,7 +34,7 @@ def test_vecenv_steps_and_autoresets():
     import torch
     from pokegym_amd.env import VecEnv
     from pokegym_amd.testrom.game import game_rom
-    env = VecEnv(128, rom=game_rom(), max_episode_steps=2, log_interval=4)
+    env = VecEnv(128, rom=game_rom(), power_on=True, max_episode_steps=2, log_interval=4)
     obs, _ = env.reset()
     assert obs.shape == (128, 72, 80, 4) and obs.device.type == "cuda"
     for t in range(4):
@@ -67,10 +72,10 @@ def test_load_state_mid_episode_keeps_step_counter():
     """load_pyboy_state leaves self.time alone (pyboy_binding.py:59-62): done fires at the same
     step with or without a state load in the middle of the episode."""
     from pokegym_amd.env import Environment
-    from pokegym_amd.testrom.game import game_rom
+    rom, state = pkbench_power_on()
     done_at = []
     for load in (False, True):
-        env = Environment(rom_path=game_rom(), max_episode_steps=5)
+        env = Environment(rom_path=rom, state_path=state, max_episode_steps=5)
         env.reset()
         first = env.load_first_state()
         for t in range(1, 8):
@@ -91,10 +96,9 @@ def test_environment_reset_takes_episode_params():
     device's seen-coordinate set."""
     import numpy as np
     from pokegym_amd.env import Environment
-    from pokegym_amd.testrom.game import game_rom
-    rom = game_rom()
-    a = Environment(rom_path=rom)
-    b = Environment(rom_path=rom, max_episode_steps=5, reward_scale=2.0)
+    rom, state = pkbench_power_on()
+    a = Environment(rom_path=rom, state_path=state)
+    b = Environment(rom_path=rom, state_path=state, max_episode_steps=5, reward_scale=2.0)
     oa, _ = a.reset(max_episode_steps=5, reward_scale=2.0)
     ob, _ = b.reset()
     assert np.array_equal(oa, ob)
@@ -114,8 +118,8 @@ def test_environment_reset_params_do_not_stick():
     """reset(max_episode_steps=X) then reset(): the reference resets both to their defaults on
     every call (environment.py:1233, :1258-1259), so the second episode has the default length."""
     from pokegym_amd.env import Environment
-    from pokegym_amd.testrom.game import game_rom
-    env = Environment(rom_path=game_rom())
+    rom, state = pkbench_power_on()
+    env = Environment(rom_path=rom, state_path=state)
     env.reset(max_episode_steps=2, reward_scale=1.0)
     assert not env.step(0)[2] and env.step(0)[2]
     env.reset()

@@ -90,9 +90,9 @@ def test_gpu_environment_info_dict_and_vecenv_info_stats():
     import torch
     from pokegym_amd.env import Environment, VecEnv
     from pokegym_amd.info import STATS_FIELDS
-    from pokegym_amd.testrom.game import game_rom
-    rom = game_rom()
-    env = Environment(rom_path=rom, max_episode_steps=3)
+    from tests.pkbench_state import pkbench_power_on
+    rom, state = pkbench_power_on()
+    env = Environment(rom_path=rom, state_path=state, max_episode_steps=3)
     env.reset()
     infos = [env.step(0)[4] for _ in range(3)]
     assert infos[0] == {} and infos[1] == {}
@@ -102,7 +102,7 @@ def test_gpu_environment_info_dict_and_vecenv_info_stats():
     assert set(STATS_FIELDS) - set(st) == {f"levels_{i}" for i in range(6)}
     assert st["coord"] == float(infos[2]["pokemon_exploration_map"].sum()) <= 3.0   # +1 per step, -1 on a map change
     env.close()
-    v = VecEnv(64, rom=rom, max_episode_steps=2, log_interval=4)
+    v = VecEnv(64, rom=rom, power_on=True, max_episode_steps=2, log_interval=4)
     v.reset()
     out = None
     for _ in range(4):
@@ -111,7 +111,7 @@ def test_gpu_environment_info_dict_and_vecenv_info_stats():
     assert info["info_records"] == 128 and info["stats"]["step"] == 2.0
     assert info["stats"]["coord"] != info["stats"]["coord"]   # NaN: no heat map kept
     v.close()
-    v = VecEnv(8, rom=rom, max_episode_steps=2, log_interval=4, heatmap=True)
+    v = VecEnv(8, rom=rom, power_on=True, max_episode_steps=2, log_interval=4, heatmap=True)
     v.reset()
     for _ in range(4):
         v.step(torch.zeros(8, dtype=torch.uint8))

@@ -42,8 +42,9 @@ def test_environment_save_video(tmp_path):
     """Environment(save_video=True): one file per episode under s_path, one frame per step, equal
     to the screens the steps produced."""
     from pokegym_amd.env import Environment
-    from pokegym_amd.testrom.game import game_rom
-    env = Environment(rom_path=game_rom(), save_video=True, max_episode_steps=4, s_path=str(tmp_path))
+    from tests.pkbench_state import pkbench_power_on
+    rom, state = pkbench_power_on()
+    env = Environment(rom_path=rom, state_path=state, save_video=True, max_episode_steps=4, s_path=str(tmp_path))
     env.reset()
     shots = []
     for a in [0, 3, 4, 1]:

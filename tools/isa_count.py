@@ -1,9 +1,10 @@
 """Static instruction counts of K1's main loop (design tool, no GPU needed).
 
 Compiles pk_step.hip for gfx950 to assembly (or reads a given .s), finds the step kernel's outer
-loop (the largest depth-1 loop), and counts the instructions laid out between its header and its
-back-edge by class.  Rare paths the compiler moved out of line (PK_RARE blocks after the loop) are
-not counted; in-line conditional blocks are, so this is an upper bound of the common path.
+loop (the depth-1 loop with the most blocks), and counts by class the instructions on its fall-through
+path from the header round to the header again (conditional branches not taken, s_branch followed).
+Rare paths the compiler moved out of line (PK_RARE blocks) are not counted; in-line conditional
+blocks are, so this is an upper bound of the common path.
 usage: python tools/isa_count.py [--prio 0|1] [--s file.s] [--blocks] [-- extra hipcc flags]"""
 import argparse
 import os
@@ -64,32 +65,40 @@ def main():
     path = a.s or compile_s(a.extra)
     lines = open(path).read().splitlines()
     K = kernel_text(lines, a.prio)
-    # loops: header labels with "Loop Header: Depth=1"; body ends at the last branch back to it
-    best = None
-    for i, l in enumerate(K):
-        m = re.match(r"^(\.LBB\d+_\d+):.*Loop Header: Depth=1", l)
-        if not m:
-            continue
-        lab = m.group(1)
-        back = [j for j in range(i, len(K)) if re.search(r"s_cbranch_\w+\s+" + re.escape(lab) + r"$", K[j].strip())]
-        if back and (best is None or back[-1] - i > best[1] - best[0]):
-            best = (i, back[-1])
-    i0, i1 = best
+    # the outer loop: the "Loop Header: Depth=1" label with the most blocks annotated as its body
+    heads = [(i, re.match(r"^\.LBB(\d+_\d+):", l).group(1)) for i, l in enumerate(K) if "Loop Header: Depth=1" in l]
+    i0, hb = max(heads, key=lambda h: sum(f"Header=BB{h[1]} Depth=1" in l for l in K))
+    labels = {re.match(r"^(\.LBB\d+_\d+):", l).group(1): i for i, l in enumerate(K) if re.match(r"^\.LBB\d+_\d+:", l)}
+    # the common path: from the header, fall through every conditional branch (in-line blocks are
+    # taken, rare blocks the compiler moved out of line are skipped) and follow s_branch, until the
+    # header comes round again (a rotated loop reaches it through a latch block laid out before it)
     cnt, blocks, cur = Counter(), [], None
-    for l in K[i0:i1 + 1]:
-        s = l.strip()
+    i, seen = i0, set()
+    while True:
+        s = K[i].strip()
+        if i == i0 and i in seen:
+            break
+        if i in seen:
+            raise SystemExit(f"walk revisits line {i}")
+        seen.add(i)
         if re.match(r"^\.LBB\d+_\d+:", s) or s.startswith("; %bb."):
             cur = [s.split()[0] if s.startswith(".") else s.split(":")[0], Counter()]
             blocks.append(cur)
+            i += 1
             continue
+        i += 1
         if not s or s.startswith(";") or s.startswith("."):
             continue
         c = classify(s)
         cnt[c] += 1
         if cur:
             cur[1][c] += 1
+        op = s.split()[0]
+        if op == "s_branch" or (op.startswith("s_cbranch") and s.split()[1] == f".LBB{hb}"):
+            i = labels[s.split()[1]]   # jumps, and the back-edge of a loop closed by a conditional branch
+    i1 = i
     tot = sum(v for k, v in cnt.items() if k not in ("waitcnt", "nop"))
-    print(f"loop body lines {i0}-{i1}: issued {tot}  " + "  ".join(f"{k} {cnt[k]}" for k in
+    print(f"loop header line {i0}, common path: issued {tot}  " + "  ".join(f"{k} {cnt[k]}" for k in
           ("valu", "salu", "branch", "lds", "vmem", "smem", "waitcnt", "nop", "misc", "other") if cnt[k]))
     if a.blocks:
         for name, c in blocks:
