@@ -747,7 +747,8 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         const u32 D = m.D;
         // the successor's secondary-op entry (read now: its LDS latency overlaps the execute stage)
         const u32 nxt = bytes >> (8u * (D & 3u));
-        const uint4 u2 = ucv2[(nxt & 0xFFu) | (D & (1u << PK_DB_NOFUSE))];
+        const u32 i2 = min((nxt & 0xFFu) | (D & (1u << PK_DB_NOFUSE)), PK_U2_NONE);
+        const uint4 u2 = ucv2[2u * i2], u2b = ucv2[2u * i2 + 1u];
         // ---------------- execute ----------------
         Ex x;
         pk_exec<PRIO>(s, c, pc, bytes, m, ev, x);
@@ -765,24 +766,35 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         // (ROM code has 4), and none of them an IO register (DIV and a folded STAT change with the clock).
         {
             const u32 len2 = u2.y & 3u;
-            // both instructions within the fetched bytes: 4 for ROM code, 3 for code in RAM
-            const bool lenok = (D & 3u) + len2 + sel(pc >= 0x8000u, 1u, 0u) <= 4u;
+            // both instructions within the fetched bytes: 4 for ROM code (and inside its 16 KiB bank:
+            // the LDS slots of other banks follow it), 3 for code in RAM
+            const u32 n2 = (D & 3u) + len2;
+            const bool lenok = sel(pc < 0x8000u, (n2 <= 4u) & ((pc & 0x3FFFu) + n2 <= 0x4000u), n2 <= 3u);
             const bool ramok = (pc < 0x8000u) | (!wr & !(pc - 0xFEFEu < 0x82u));
             const u32 lim = sel(s.lcd0 & 0x80u, s.target, FRAME_CYCLES);   // next LCD event / LCD-off frame end
             const bool fuse = (len2 != 0u) & ((int)cycles < slack) & (s.clock + cycles < lim)
                             & !(s.tim0 & (4u << 24)) & !(wr & !wram) & ramok & lenok;
             const u32 M2 = sel(fuse, u2.y, PK_U2_NONE_Y);
-            // operand (pair, or register in byte 0) + delta; INC/DEC r flags: Z N H replace F's bits
-            // under the entry's mask, C kept; val2 = r16 | F' << 16 | r8 << 24 through the selectors
-            const u32 x = perm(s.w1, s.w0, u2.x);
-            const int dl = sfield(M2, PK_U2B_DELTA, 8);
-            const u32 r = x + (u32)dl;
-            const u32 nz = sel((r & 0xFFu) == 0u, 0x80u, 0u) | ((u32)dl & 0x40u);
-            const u32 zh = nz | (((x ^ r) << 1) & ~0xC0u);   // Z N from nz, H = carry into bit 4
+            // X (pair, or register in byte 0); Y = register | immediate n, ^ the subtract mask, + delta;
+            // one adder X + Y + carry-in (ADC/SBC: F.C; SUB/SBC/CP: ^ 1), a logic unit (AND XOR OR),
+            // flags Z from the result, H/C from the carry vector; F' replaces F's bits under the
+            // entry's mask; val2 = r16 | F' << 16 | r8 << 24 through the selectors
+            const u32 ctl = u2b.w;
             const u32 F1 = (s.w1 >> 16) & 0xFFu;
+            const u32 x = perm(s.w1, s.w0, u2.x);
+            const u32 yv = (perm(s.w1, s.w0, u2b.x) | ((nxt >> 8) & u2b.y)) ^ u2b.z;
+            const u32 yy = yv + (u32)sfield(M2, PK_U2B_DELTA, 8);
+            const u32 cin = (bit(F1, 4) & ctl) ^ bit(ctl, PK_U2C_SUBC);
+            const u32 r = x + yy + cin;
+            const u32 cvec = x ^ yy ^ r;
+            const u32 hc = ((cvec << 1) & 0x20u) | ((cvec >> 4) & 0x10u);   // H: carry into bit 4, C: into bit 8
+            const u32 lr = (x & yv & (0u - bit(ctl, PK_U2C_LA))) | ((x ^ yv) & (0u - bit(ctl, PK_U2C_LX)));
+            const u32 res = sel(ctl & (1u << PK_U2C_LOGIC), lr, r);
+            const u32 comp = sel((res & 0xFFu) == 0u, 0x80u, 0u) | ((hc ^ (ctl >> PK_U2C_FLIP)) & (ctl >> PK_U2C_HCM))
+                           | (ctl >> PK_U2C_FCONST);
             const u32 fm = M2 >> PK_U2B_FM;
-            const u32 Fn = (zh & fm) | (F1 & ~fm);
-            const u32 val2 = perm(Fn, r, 0x00040100u);
+            const u32 Fn = (comp & fm) | (F1 & ~fm);
+            const u32 val2 = perm(Fn, res, 0x00040100u);
             const u32 w0f = perm(val2, s.w0, sel(fuse, u2.z, PK_S0_ID));
             const u32 w1f = perm(val2, s.w1, sel(fuse, u2.w, PK_S1_ID));
             // JR: taken when (F & mask) == cv (mask at F's byte of the x word, cv at the same byte of

@@ -46,10 +46,12 @@ enum { PK_UE_D = 0, PK_UE_U, PK_UE_K, PK_UE_V, PK_UE_XR, PK_UE_XE, PK_UE_YR, PK_
 #define PK_UC_INT 512u    // pseudo-op: interrupt dispatch (push PC, jump to the vector)
 #define PK_UC_IDLE 513u   // pseudo-op: halted / crashed CPU, 4 cycles
 #define PK_UC_NOP0 514u   // pseudo-op: interrupt pending with IME off (queued), 0 cycles
-// secondary-op table (fused pairs, see pk_u2_entry): 512 entries x 4 dwords after the main table
-#define PK_U2_WORDS 4u
+// secondary-op table (fused pairs, see pk_u2_entry): 257 entries x 8 dwords after the main table
+// (entry 256 is empty: the index of every primary that may not fuse)
+#define PK_U2_WORDS 8u
+#define PK_U2_NONE 256u
 #define PK_UC_U2 (PK_UC_ENTRIES * PK_UE_WORDS)
-#define PK_UC_WORDS (PK_UC_U2 + 512u * PK_U2_WORDS)
+#define PK_UC_WORDS (PK_UC_U2 + (PK_U2_NONE + 1u) * PK_U2_WORDS)
 
 // D word: memory, timing, control
 #define PK_DB_LEN 0       // 2 bits  instruction length
@@ -580,44 +582,89 @@ static inline void pk_store_uop(uint32_t* e, PkUop o, bool real) {
 // ---- secondary ops: fused into the iteration of the instruction before them ----
 // The SIMT loop pays for one iteration per emulated instruction whatever the instruction, so the
 // cheap register-only successors of an instruction run in the same iteration: a JR (cc), LD r,r',
-// INC/DEC r, INC/DEC BC/DE/HL or NOP right after a fusable instruction executes on the registers
-// and flags that instruction left, exactly as the next cpu.tick would, when nothing can happen in
-// between (pk_step.hip states the test).  The table has 512 entries: index = opcode | the primary's
-// PK_DB_NOFUSE bit (entries 256-511 are empty).  Entry: x = operand selector over w1:w0 (the pair,
-// or the source/target register, into byte 0), y = misc (length, cycles, JR condition, delta, flag
-// mask), z/w = writeback selectors of val2 = r16 | F' << 16 | r8 << 24 (as S0/S1).
+// LD r,n, INC/DEC r, INC/DEC BC/DE/HL, an 8-bit ALU op on A with a register or immediate operand
+// (ADD ADC SUB SBC AND XOR OR CP), CPL, SCF or NOP right after a fusable instruction executes on
+// the registers and flags that instruction left, exactly as the next cpu.tick would, when nothing
+// can happen in between (pk_step.hip states the test).  Index = opcode, or PK_U2_NONE (empty) for a
+// primary with PK_DB_NOFUSE.  Entry, two uint4:
+//   a.x  X selector over w1:w0 (the pair, or a register into byte 0; JR: the F mask at F's byte)
+//   a.y  misc: length, cycles, delta, JR condition value, mask of the F bits the op writes
+//   a.z/a.w  writeback selectors of val2 = res16 | F' << 16 | res8 << 24 (as S0/S1)
+//   b.x  Y selector over w1:w0 (register operand), b.y immediate mask (Y |= n & b.y), b.z Y xor
+//        mask (0xFF: subtract), b.w control (PK_U2C_*)
+// datapath: r = X + (Y ^ b.z) + delta + carry-in; res = r, or the logic unit's X&Y / X^Y / X|Y;
+// flags Z from res, H/C from the adder's carry vector (^ flip, & mask), constants ORed in.
 #define PK_U2B_LEN 0      // 2 bits length (0: no secondary op)
 #define PK_U2B_ONE 2      // 1: counts as an executed instruction
 #define PK_U2B_CYC 4      // 4 bits cycles/4 (JR: not taken)
-#define PK_U2B_DELTA 8    // 8 bits signed: r = operand + delta (INC/DEC)
+#define PK_U2B_DELTA 8    // 8 bits signed: added to Y (INC/DEC)
 #define PK_U2B_CV 16      // 8 bits: JR taken when (F & mask) == cv, the mask in byte 2 of the x word;
                           //         1 for every other entry (F's low nibble is 0: never)
-#define PK_U2B_FM 24      // 8 bits: F bits replaced by Z N H (INC/DEC r: 0xE0), the rest kept
+#define PK_U2B_FM 24      // 8 bits: F bits the op writes, the rest kept
 #define PK_U2_NONE_Y (1u << PK_U2B_CV)
+#define PK_U2C_USEC 0     // carry-in F.C (ADC, SBC)
+#define PK_U2C_SUBC 1     // carry-in ^ 1 (SUB, SBC, CP: X + ~Y + 1 [- C])
+#define PK_U2C_LOGIC 2    // res = logic unit
+#define PK_U2C_LA 3       // logic includes X & Y (AND, OR)
+#define PK_U2C_LX 4       // logic includes X ^ Y (XOR, OR, CPL)
+#define PK_U2C_FCONST 8   // 8 bits: F bits set (N of SUB/DEC/CP, H of AND, CPL/SCF constants)
+#define PK_U2C_HCM 16     // 8 bits: F bits taken from the adder (H 0x20, C 0x10)
+#define PK_U2C_FLIP 24    // 8 bits: adder flags inverted (borrow = !carry)
 static inline void pk_u2_entry(uint32_t* e, int op) {
-    uint32_t len = 0, cyc = 0, cv = 1, fm = 0;
+    uint32_t len = 0, cyc = 0, cv = 1, fm = 0, ysel = PK_PZERO, imm = 0, ysm = 0, ctl = 0;
     int delta = 0;
     PkUop o = pk_uop_base(1, 4);   // identity writeback selectors (F from val2 = F' = F unless fm)
     uint32_t sel = PK_PZERO;
+    const int src = op & 7, dst = (op >> 3) & 7;
     if (op < 256) {
         if (op == 0x00) {
             len = 1; cyc = 4;
-        } else if (op >= 0x40 && op < 0x80 && op != 0x76 && (op & 7) != 6 && ((op >> 3) & 7) != 6) {  // LD r, r'
+        } else if (op >= 0x40 && op < 0x80 && op != 0x76 && src != 6 && dst != 6) {  // LD r, r'
             len = 1; cyc = 4;
-            sel = pk_sel8(op & 7);
-            pk_wb_r8(o, (op >> 3) & 7);
-        } else if ((op & 0xC6) == 0x04 && ((op >> 3) & 7) != 6) {  // INC r / DEC r: Z N H, C kept
-            const int r = (op >> 3) & 7;
+            sel = pk_sel8(src);
+            pk_wb_r8(o, dst);
+        } else if ((op & 0xC7) == 0x06 && dst != 6) {  // LD r, n
+            len = 2; cyc = 8;
+            imm = 0xFFu;
+            pk_wb_r8(o, dst);
+        } else if ((op & 0xC6) == 0x04 && dst != 6) {  // INC r / DEC r: Z N H, C kept
             len = 1; cyc = 4; fm = 0xE0;
-            sel = pk_sel8(r);
+            sel = pk_sel8(dst);
             delta = (op & 1) ? -1 : 1;
-            pk_wb_r8(o, r);
+            ctl = pk_fld(PK_F_H, PK_U2C_HCM) | ((op & 1) ? pk_fld(PK_F_H, PK_U2C_FLIP) | pk_fld(PK_F_N, PK_U2C_FCONST) : 0u);
+            pk_wb_r8(o, dst);
         } else if ((op & 0xC7) == 0x03 && ((op >> 4) & 3) != 3) {  // INC rr / DEC rr (BC DE HL), no flags
             const int p = (op >> 4) & 3;
             len = 1; cyc = 8;
             sel = pk_sel16(p);
             delta = (op & 8) ? -1 : 1;
             pk_wb_r16(o, p);
+        } else if ((op >= 0x80 && op < 0xC0 && src != 6) || (op & 0xC7) == 0xC6) {  // ALU A, r / ALU A, n
+            const int f = dst;   // ADD ADC SUB SBC AND XOR OR CP
+            const bool immop = op >= 0xC0;
+            len = immop ? 2 : 1; cyc = immop ? 8 : 4; fm = 0xF0;
+            sel = pk_sel8(7);
+            if (immop) imm = 0xFFu;
+            else ysel = pk_sel8(src);
+            if (f < 4 || f == 7) {   // adder: Z N H C
+                const bool sub = f == 2 || f == 3 || f == 7;
+                ysm = sub ? 0xFFu : 0u;
+                ctl = pk_fld(PK_F_H | PK_F_C, PK_U2C_HCM) | ((f == 1 || f == 3) ? pk_fld(1, PK_U2C_USEC) : 0u)
+                    | (sub ? pk_fld(1, PK_U2C_SUBC) | pk_fld(PK_F_H | PK_F_C, PK_U2C_FLIP) | pk_fld(PK_F_N, PK_U2C_FCONST) : 0u);
+            } else {                 // logic: Z 0 H(AND) 0
+                ctl = pk_fld(1, PK_U2C_LOGIC) | (f != 5 ? pk_fld(1, PK_U2C_LA) : 0u) | (f != 4 ? pk_fld(1, PK_U2C_LX) : 0u)
+                    | (f == 4 ? pk_fld(PK_F_H, PK_U2C_FCONST) : 0u);
+            }
+            if (f != 7) pk_wb_r8(o, 7);
+        } else if (op == 0x2F) {  // CPL: A ^ 0xFF, N H set
+            len = 1; cyc = 4; fm = PK_F_N | PK_F_H;
+            sel = pk_sel8(7);
+            ysm = 0xFFu;
+            ctl = pk_fld(1, PK_U2C_LOGIC) | pk_fld(1, PK_U2C_LX) | pk_fld(PK_F_N | PK_F_H, PK_U2C_FCONST);
+            pk_wb_r8(o, 7);
+        } else if (op == 0x37) {  // SCF: N H cleared, C set
+            len = 1; cyc = 4; fm = PK_F_N | PK_F_H | PK_F_C;
+            ctl = pk_fld(PK_F_C, PK_U2C_FCONST);
         } else if (op == 0x18 || op == 0x20 || op == 0x28 || op == 0x30 || op == 0x38) {  // JR (cc,) e
             static const uint32_t msk[4] = {0x80, 0x80, 0x10, 0x10}, val[4] = {0, 0x80, 0, 0x10};  // NZ Z NC C
             len = 2; cyc = 8;   // + 4 when taken
@@ -630,6 +677,10 @@ static inline void pk_u2_entry(uint32_t* e, int op) {
          | (((uint32_t)delta & 0xFFu) << PK_U2B_DELTA) | (cv << PK_U2B_CV) | (fm << PK_U2B_FM);
     e[2] = o.s0;
     e[3] = o.s1;
+    e[4] = ysel;
+    e[5] = imm;
+    e[6] = ysm;
+    e[7] = ctl;
 }
 
 static inline void pk_build_ucode(uint32_t* t /* PK_UC_WORDS */) {
@@ -646,5 +697,5 @@ static inline void pk_build_ucode(uint32_t* t /* PK_UC_WORDS */) {
     PkUop idle = pk_uop_base(0, 4), nop0 = pk_uop_base(0, 0);
     const PkUop ps[3] = {it, idle, nop0};
     for (int j = 0; j < 3; j++) pk_store_uop(t + (size_t)(512 + j) * PK_UE_WORDS, ps[j], false);
-    for (int op = 0; op < 512; op++) pk_u2_entry(t + PK_UC_U2 + (size_t)op * PK_U2_WORDS, op);
+    for (int op = 0; op <= (int)PK_U2_NONE; op++) pk_u2_entry(t + PK_UC_U2 + (size_t)op * PK_U2_WORDS, op);
 }
