@@ -25,9 +25,9 @@ hipError_t pk_launch_render(const PkStepArgs& a, hipStream_t s);
 hipError_t pk_launch_reset(const PkResetArgs& a, hipStream_t s);
 hipError_t pk_launch_list(const uint8_t* mask, uint32_t env0, uint32_t env1, uint32_t* cnt, uint32_t* ids, hipStream_t s);
 hipError_t pk_launch_render_latched(const PkStepArgs& a, hipStream_t s);
-hipError_t pk_launch_gather_env(const uint8_t* mem, uint32_t env, uint8_t* out, hipStream_t s);
-hipError_t pk_launch_gather_range(const uint8_t* mem, uint32_t env0, uint32_t count, uint8_t* out, hipStream_t s);
-hipError_t pk_launch_scatter_env(uint8_t* mem, uint32_t env, const uint8_t* in, hipStream_t s);
+hipError_t pk_launch_gather_env(const uint8_t* mem, uint32_t env, uint32_t sh, uint8_t* out, hipStream_t s);
+hipError_t pk_launch_gather_range(const uint8_t* mem, uint32_t env0, uint32_t count, uint32_t sh, uint8_t* out, hipStream_t s);
+hipError_t pk_launch_scatter_env(uint8_t* mem, uint32_t env, uint32_t sh, const uint8_t* in, hipStream_t s);
 hipError_t pk_launch_done(const uint32_t* time_reg, uint32_t n, uint32_t max_steps, uint8_t* term,
                           uint8_t* trunc, double* rew, hipStream_t s);
 hipError_t pk_launch_reward(const PkRewardArgs& a, hipStream_t s);
@@ -36,7 +36,7 @@ hipError_t pk_launch_rreset_post(const PkRewardArgs& a, hipStream_t s);
 hipError_t pk_launch_obs(const PkRewardArgs& a, hipStream_t s);
 hipError_t pk_launch_seen_rehash(const uint32_t* old_tab, uint32_t old_lg, uint32_t* new_tab, uint32_t new_lg,
                                  const uint32_t* rs, uint32_t n, uint32_t np, hipStream_t s);
-hipError_t pk_launch_ram_copy(uint8_t* mem, uint8_t* dense, uint32_t n, uint32_t phys0, uint32_t len,
+hipError_t pk_launch_ram_copy(uint8_t* mem, uint8_t* dense, uint32_t n, uint32_t sh, uint32_t phys0, uint32_t len,
                               uint32_t to_dense, hipStream_t s);
 
 namespace {
@@ -227,6 +227,7 @@ struct pk_handle {
     uint32_t wave_lanes = 0;   // envs per wave in K1: 0 = by launch size (k1_wave_lanes), else PK_WAVE_LANES
     uint32_t simds = 1024;     // SIMDs of the device (4 per CU)
     uint32_t k1_block = 0;     // K1 workgroup size override (PK_K1_BLOCK), 0 = by geometry
+    uint32_t ilv_sh = 6;       // RAM image interleave 1 << ilv_sh (pk_layout.h pk_img_off): K1's envs per wave
     int k1_prio = -1;          // K1 wave-priority variant override (PK_K1_PRIO 0/1), -1 = by shape
     uint32_t frames = 24, release = 8, flags = 0, max_steps = 20480;
     uint32_t mbc = 3, bank_mask = 0;
@@ -307,6 +308,8 @@ void pk_destroy(pk_handle* h) {
     delete h;
 }
 
+static uint32_t k1_wave_lanes(const struct pk_handle* h, uint32_t count);
+
 int pk_create(const pk_config* cfg, pk_handle** out) {
     if (!cfg || !out) return fail(-EINVAL, "null argument");
     *out = nullptr;
@@ -351,6 +354,18 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
             h->k1_block = (uint32_t)v;
         }
         if (const char* pr = getenv("PK_K1_PRIO")) h->k1_prio = atoi(pr) ? 1 : 0;
+        // image interleave = K1's envs per wave for this handle (no 64-byte line shared by two
+        // waves; a wave's lanes share one sub-block base); PK_ILV (>= the wave's envs) overrides
+        uint32_t ilv = k1_wave_lanes(h, h->n);
+        if (const char* iv = getenv("PK_ILV")) {
+            int v = atoi(iv);
+            if (v < 1 || v > 64 || (v & (v - 1)) || (uint32_t)v < ilv) {
+                delete h;
+                return fail(-EINVAL, "PK_ILV must be a power of two <= 64 and >= K1's envs per wave (%u)", ilv);
+            }
+            ilv = (uint32_t)v;
+        }
+        h->ilv_sh = (uint32_t)__builtin_ctz(ilv);
     }
     h->frames = cfg->frame_skip;
     h->release = cfg->release_frame;
@@ -470,7 +485,7 @@ static PkRewardArgs reward_args(pk_handle* h, uint32_t env0, uint32_t env1) {
     r.info = h->info; r.info_flag = h->info_flag; r.heat = h->heat; r.info_bits = h->info_bits;
     r.reward_scale = h->reward_scale; r.n = h->n; r.npad = h->npad; r.cap_log2 = h->cap_log2;
     r.max_steps = h->max_steps; r.reload_always = (h->flags & PK_F_RELOAD_ON_RESET) ? 1 : 0;
-    r.env0 = env0; r.env1 = env1;
+    r.env0 = env0; r.env1 = env1; r.ilv_sh = h->ilv_sh;
     return r;
 }
 
@@ -493,7 +508,7 @@ static int template_reset(pk_handle* h, const uint8_t* mask, uint32_t env0, uint
     a.mem = h->mem; a.regs = h->regs; a.lat = h->lat; a.screen = h->screen;
     a.tmpl_mem = h->t_mem; a.tmpl_regs = h->t_regs; a.tmpl_lat = h->t_lat; a.tmpl_screen = h->t_screen;
     a.cnt = list_cnt(h, env0, 0); a.ids = list_ids(h, env0, 0); a.n = h->n; a.npad = h->npad;
-    a.lat_stride = (uint32_t)h->lat_stride; a.env0 = env0; a.env1 = env1;
+    a.lat_stride = (uint32_t)h->lat_stride; a.env0 = env0; a.env1 = env1; a.ilv_sh = h->ilv_sh;
     HIPCHK(pk_launch_reset(a, s));
     return 0;
 }
@@ -538,7 +553,7 @@ int pk_get_ram(pk_handle* h, uint16_t addr, uint32_t len, uint8_t* dense, void* 
     if (wram && (addr & 0x1FFF) + len > 0x2000) return fail(-EINVAL, "pk_get_ram: range wraps the echo mirror");
     HIPCHK(hipSetDevice(h->device));
     uint32_t phys0 = wram ? PK_P_WRAM + (addr & 0x1FFFu) : PK_P_HRAM + (addr - 0xFF80u);
-    HIPCHK(pk_launch_ram_copy(h->mem, dense, h->n, phys0, len, 1, (hipStream_t)stream));
+    HIPCHK(pk_launch_ram_copy(h->mem, dense, h->n, h->ilv_sh, phys0, len, 1, (hipStream_t)stream));
     return 0;
 }
 
@@ -549,7 +564,7 @@ int pk_set_ram(pk_handle* h, uint16_t addr, uint32_t len, const uint8_t* dense, 
     if (wram && (addr & 0x1FFF) + len > 0x2000) return fail(-EINVAL, "pk_set_ram: range wraps the echo mirror");
     HIPCHK(hipSetDevice(h->device));
     uint32_t phys0 = wram ? PK_P_WRAM + (addr & 0x1FFFu) : PK_P_HRAM + (addr - 0xFF80u);
-    HIPCHK(pk_launch_ram_copy(h->mem, const_cast<uint8_t*>(dense), h->n, phys0, len, 0, (hipStream_t)stream));
+    HIPCHK(pk_launch_ram_copy(h->mem, const_cast<uint8_t*>(dense), h->n, h->ilv_sh, phys0, len, 0, (hipStream_t)stream));
     return 0;
 }
 
@@ -606,6 +621,7 @@ static PkStepArgs step_args(pk_handle* h, const uint8_t* actions, uint32_t env0,
     a.simds = h->simds;
     a.dbg = h->dbg;
     a.env0 = env0; a.env1 = env1;
+    a.ilv_sh = h->ilv_sh;
     return a;
 }
 
@@ -660,7 +676,7 @@ static int fetch_env(pk_handle* h, uint32_t env, std::vector<uint8_t>& mem, uint
     if (env >= h->n) return fail(-EINVAL, "env %u out of range (n=%u)", env, h->n);
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(pk_launch_gather_env(h->mem, env, h->scratch, nullptr));
+    HIPCHK(pk_launch_gather_env(h->mem, env, h->ilv_sh, h->scratch, nullptr));
     mem.resize(PK_PHYS);
     HIPCHK(hipMemcpy(mem.data(), h->scratch, PK_PHYS, hipMemcpyDeviceToHost));
     for (uint32_t f = 0; f < PK_NREGS; f++)
@@ -703,7 +719,7 @@ int pk_snapshot_range(pk_handle* h, uint32_t env0, uint32_t count, uint8_t* out,
     int rc = 0;
     for (uint32_t c0 = 0; c0 < count && !rc; c0 += chunk) {
         const uint32_t e0 = env0 + c0, m = (count - c0) < chunk ? (count - c0) : chunk;
-        hipError_t e = pk_launch_gather_range(h->mem, e0, m, dmem, nullptr);
+        hipError_t e = pk_launch_gather_range(h->mem, e0, m, h->ilv_sh, dmem, nullptr);
         if (e == hipSuccess) e = hipMemcpy(mem.data(), dmem, (size_t)m * PK_PHYS, hipMemcpyDeviceToHost);
         for (uint32_t f = 0; f < PK_NREGS && e == hipSuccess; f++)
             e = hipMemcpy(&regs[(size_t)f * chunk], h->regs + (size_t)f * h->npad + e0, (size_t)m * 4, hipMemcpyDeviceToHost);
@@ -739,7 +755,7 @@ int pk_load_env(pk_handle* h, uint32_t env, const uint8_t* in, uint64_t len) {
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(h->scratch, t.mem.data(), PK_PHYS, hipMemcpyHostToDevice));
-    HIPCHK(pk_launch_scatter_env(h->mem, env, h->scratch, nullptr));
+    HIPCHK(pk_launch_scatter_env(h->mem, env, h->ilv_sh, h->scratch, nullptr));
     HIPCHK(hipDeviceSynchronize());
     // machine state only: the env's step counter (PK_R_TIME, pokegym `self.time`) and the per-step
     // bookkeeping slots survive a load, as in load_pyboy_state (pyboy_binding.py:59-62), which
@@ -838,13 +854,12 @@ int pk_poke(pk_handle* h, uint32_t env, uint16_t addr, uint32_t len, const uint8
     uint32_t regs[PK_NREGS], lat[3 * PK_ROWS];
     int rc = fetch_env(h, env, mem, regs, lat, screen);
     if (rc) return rc;
-    uint32_t gid = env / PK_LANES, lane = env % PK_LANES;
     for (uint32_t i = 0; i < len; i++) {
         uint32_t a = (uint32_t)addr + i, phys;
         int special;
         if (guest_phys(a, regs, h->mbc, &phys, &special) != 0)
             return fail(-ENOTSUP, "pk_poke supports RAM regions only (addr 0x%04x)", a);
-        HIPCHK(hipMemcpy(h->mem + (size_t)gid * PK_GROUP_STRIDE + (size_t)phys * PK_LANES + lane, &in[i], 1,
+        HIPCHK(hipMemcpy(h->mem + pk_img_off(env, phys, h->ilv_sh), &in[i], 1,
                          hipMemcpyHostToDevice));
     }
     return 0;

@@ -35,9 +35,7 @@ __global__ void __launch_bounds__(64) pk_render_kernel(PkStepArgs A) {
         return;
     }
     if (!(l2 & 0x100u)) return;
-    Mem m;
-    m.g = A.mem + (size_t)gid * PK_GROUP_STRIDE;
-    m.lane = lane;
+    const Mem m = mem_view(A.mem, env, A.ilv_sh);
     render_line(m, y, A.lat[idx], A.lat[A.lat_stride + idx], (int)(l2 & 0xFFu) - 1, out);
     A.lat[2u * A.lat_stride + idx] = l2 & ~0x100u;
 }
@@ -79,8 +77,8 @@ __global__ void __launch_bounds__(256) pk_reset_mem_kernel(PkResetArgs A) {
     const u32 cnt = *A.cnt;
     for (u32 k = threadIdx.x; k < cnt; k += blockDim.x) {
         const u32 env = A.ids[k];
-        u8* g = A.mem + (size_t)(env / PK_LANES) * PK_GROUP_STRIDE + env % PK_LANES;
-        for (u32 p = blockIdx.x; p < PK_PHYS; p += gridDim.x) g[(size_t)p * PK_LANES] = A.tmpl_mem[p];
+        const Mem m = mem_view(A.mem, env, A.ilv_sh);
+        for (u32 p = blockIdx.x; p < PK_PHYS; p += gridDim.x) st_phys(m, p, A.tmpl_mem[p]);
     }
 }
 
@@ -100,29 +98,27 @@ __global__ void __launch_bounds__(256) pk_reset_regs_kernel(PkResetArgs A) {
 }
 
 // gather one env's RAM image into a compact buffer (for pk_snapshot / pk_peek)
-__global__ void pk_gather_env_kernel(const u8* mem, u32 env, u8* out) {
-    const u32 gid = env / PK_LANES, lane = env % PK_LANES;
-    const u8* g = mem + (size_t)gid * PK_GROUP_STRIDE;
+__global__ void pk_gather_env_kernel(const u8* mem, u32 env, u32 sh, u8* out) {
+    const Mem m = mem_view(const_cast<u8*>(mem), env, sh);
     for (u32 p = blockIdx.x * blockDim.x + threadIdx.x; p < PK_PHYS; p += gridDim.x * blockDim.x)
-        out[p] = g[p * PK_LANES + lane];
+        out[p] = ld_phys(m, p);
 }
 
 // gather envs [env0, env0 + count) into out[count][PK_PHYS] (bulk snapshots): one thread per
-// (phys row, env) with env fastest, so each wave reads 64 consecutive interleaved bytes
-__global__ void __launch_bounds__(256) pk_gather_range_kernel(const u8* mem, u32 env0, u32 count, u8* out) {
+// (phys row, env) with env fastest, so each wave reads consecutive interleaved bytes
+__global__ void __launch_bounds__(256) pk_gather_range_kernel(const u8* mem, u32 env0, u32 count, u32 sh, u8* out) {
     const size_t total = (size_t)count * PK_PHYS;
     for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
         const u32 k = (u32)(t % count), p = (u32)(t / count);
         const u32 env = env0 + k;
-        out[(size_t)k * PK_PHYS + p] = mem[(size_t)(env / PK_LANES) * PK_GROUP_STRIDE + (size_t)p * PK_LANES + env % PK_LANES];
+        out[(size_t)k * PK_PHYS + p] = mem[pk_img_off(env, p, sh)];
     }
 }
 
-__global__ void pk_scatter_env_kernel(u8* mem, u32 env, const u8* in) {
-    const u32 gid = env / PK_LANES, lane = env % PK_LANES;
-    u8* g = mem + (size_t)gid * PK_GROUP_STRIDE;
+__global__ void pk_scatter_env_kernel(u8* mem, u32 env, u32 sh, const u8* in) {
+    const Mem m = mem_view(mem, env, sh);
     for (u32 p = blockIdx.x * blockDim.x + threadIdx.x; p < PK_PHYS; p += gridDim.x * blockDim.x)
-        g[p * PK_LANES + lane] = in[p];
+        st_phys(m, p, in[p]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -154,18 +150,18 @@ hipError_t pk_launch_reset(const PkResetArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t pk_launch_gather_env(const u8* mem, u32 env, u8* out, hipStream_t s) {
-    hipLaunchKernelGGL(pk_gather_env_kernel, dim3(64), dim3(256), 0, s, mem, env, out);
+hipError_t pk_launch_gather_env(const u8* mem, u32 env, u32 sh, u8* out, hipStream_t s) {
+    hipLaunchKernelGGL(pk_gather_env_kernel, dim3(64), dim3(256), 0, s, mem, env, sh, out);
     return hipGetLastError();
 }
 
-hipError_t pk_launch_gather_range(const u8* mem, u32 env0, u32 count, u8* out, hipStream_t s) {
-    hipLaunchKernelGGL(pk_gather_range_kernel, dim3(2048), dim3(256), 0, s, mem, env0, count, out);
+hipError_t pk_launch_gather_range(const u8* mem, u32 env0, u32 count, u32 sh, u8* out, hipStream_t s) {
+    hipLaunchKernelGGL(pk_gather_range_kernel, dim3(2048), dim3(256), 0, s, mem, env0, count, sh, out);
     return hipGetLastError();
 }
 
-hipError_t pk_launch_scatter_env(u8* mem, u32 env, const u8* in, hipStream_t s) {
-    hipLaunchKernelGGL(pk_scatter_env_kernel, dim3(64), dim3(256), 0, s, mem, env, in);
+hipError_t pk_launch_scatter_env(u8* mem, u32 env, u32 sh, const u8* in, hipStream_t s) {
+    hipLaunchKernelGGL(pk_scatter_env_kernel, dim3(64), dim3(256), 0, s, mem, env, sh, in);
     return hipGetLastError();
 }
 

@@ -1,12 +1,15 @@
 // pk_layout.h — device data layout shared by the HIP kernels and the host C-ABI.
 //
-// One wavefront lane = one emulator ("env").  Envs are grouped 64 to a "group" (= one wave).
+// One wavefront lane = one emulator ("env").  Envs are grouped 64 to a "group".
 //
-// Per-env RAM image ("phys" address space, PK_PHYS bytes), stored LANE-INTERLEAVED per group:
-//     byte(env, phys) = mem[group(env) * PK_GROUP_STRIDE + phys * 64 + lane(env)]
-// so the 64 lanes of a wave touching the same guest address (the common case while they run
-// the same code) hit 64 consecutive bytes — one coalesced access — and a group's whole state is
-// one contiguous 3.0 MiB block of HBM.
+// Per-env RAM image ("phys" address space, PK_PHYS bytes), stored LANE-INTERLEAVED per group, with
+// an interleave W = 1 << sh (sh <= 6) chosen per handle = K1's envs per wave (16, 32 or 64): a
+// group's PK_GROUP_STRIDE bytes hold 64 / W sub-blocks of W envs, and inside a sub-block
+//     byte(env, phys) = sub-block base[phys * W + env % W]          (pk_img_off)
+// so the W lanes of a wave touching the same guest address (the common case while they run the
+// same code) hit W consecutive bytes — one coalesced access — no 64-byte line is shared by two
+// waves, and a 128-byte line holds 128 / W consecutive guest bytes of the wave's envs.  (W = 64 is
+// the round-1/2 layout.)
 //
 //   phys 0x0000-0x1FFF  VRAM   (guest 0x8000-0x9FFF)
 //   phys 0x2000-0x3FFF  WRAM   (guest 0xC000-0xDFFF, echo 0xE000-0xFDFF)
@@ -20,6 +23,7 @@
 // Per-env lane registers: SoA u32 arrays regs[field * npad + env] (coalesced load/store at
 // kernel entry/exit; inside the kernel they live in VGPRs).
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 typedef struct { uint32_t x, y; } uint2_t;
@@ -27,6 +31,12 @@ typedef struct { uint32_t x, y; } uint2_t;
 #define PK_LANES 64u
 #define PK_PHYS 0xC200u
 #define PK_GROUP_STRIDE (PK_PHYS * PK_LANES)
+
+// byte offset of (env, phys) in the image array, interleave 1 << sh
+__host__ __device__ static inline uint64_t pk_img_off(uint32_t env, uint32_t phys, uint32_t sh) {
+    const uint32_t l = env & (PK_LANES - 1u);
+    return (uint64_t)(env / PK_LANES) * PK_GROUP_STRIDE + (((uint64_t)(l >> sh) * PK_PHYS + phys) << sh) + (l & ((1u << sh) - 1u));
+}
 
 #define PK_P_VRAM 0x0000u
 #define PK_P_WRAM 0x2000u
@@ -95,6 +105,7 @@ struct PkStepArgs {
     uint32_t prio;            // K1 wave-priority variant (two waves per SIMD; PK_K1_PRIO overrides)
     unsigned long long* dbg;  // diagnostic counters (-DPK_STAMP builds only), else null
     uint32_t env0, env1;      // env range of this launch: [env0, env1), env0 % 64 == 0 (sub-batches)
+    uint32_t ilv_sh;          // image interleave: 1 << ilv_sh envs (pk_img_off)
 };
 
 struct PkResetArgs {
@@ -110,4 +121,5 @@ struct PkResetArgs {
     const uint32_t* ids;         // ... and their ids (pk_list_kernel)
     uint32_t n, npad, lat_stride;
     uint32_t env0, env1;         // env range the list was built over
+    uint32_t ilv_sh;             // image interleave (pk_img_off)
 };

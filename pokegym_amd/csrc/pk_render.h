@@ -16,13 +16,22 @@ typedef uint8_t u8;
 __device__ __forceinline__ u32 bfe8(u32 v, u32 sh) { return (v >> sh) & 0xFFu; }
 __device__ __forceinline__ u32 setb8(u32 v, u32 sh, u32 b) { return (v & ~(0xFFu << sh)) | ((b & 0xFFu) << sh); }
 
-// per-lane view of a lane-interleaved RAM image: byte(phys) = g[phys * 64 + lane]
+// per-lane view of a lane-interleaved RAM image (pk_layout.h): byte(phys) = g[phys << sh | lane]
 struct Mem {
-    u8* g;      // group base (wave-uniform)
-    u32 lane;
+    u8* g;      // the env's sub-block base
+    u32 lane;   // lane within the sub-block
+    u32 sh;     // interleave shift
 };
-__device__ __forceinline__ u32 ld_phys(const Mem& m, u32 phys) { return m.g[phys * PK_LANES + m.lane]; }
-__device__ __forceinline__ void st_phys(const Mem& m, u32 phys, u32 v) { m.g[phys * PK_LANES + m.lane] = (u8)v; }
+__device__ __forceinline__ u32 ld_phys(const Mem& m, u32 phys) { return m.g[(phys << m.sh) + m.lane]; }
+__device__ __forceinline__ void st_phys(const Mem& m, u32 phys, u32 v) { m.g[(phys << m.sh) + m.lane] = (u8)v; }
+// the view of env (interleave shift sh)
+__device__ __forceinline__ Mem mem_view(u8* mem, u32 env, u32 sh) {
+    Mem m;
+    m.g = mem + pk_img_off(env, 0u, sh) - (env & (PK_LANES - 1u) & ((1u << sh) - 1u));
+    m.lane = env & (PK_LANES - 1u) & ((1u << sh) - 1u);
+    m.sh = sh;
+    return m;
+}
 
 // grey shade of palette index 0..3 (0xFF 0x99 0x55 0x00)
 __device__ __forceinline__ u32 grey(u32 shade) { return (0x005599FFu >> (8u * shade)) & 0xFFu; }
@@ -133,10 +142,12 @@ __device__ inline void render_line(const Mem& m, u32 y, u32 lat0, u32 lat1, int 
 
 // rasterise every latched-but-pending line of this lane now (before VRAM/OAM change).  Rare
 // path: kept out of line with by-value arguments so the step loop's state stays in VGPRs.
-__device__ __noinline__ static void flush_lines(u32* lat, u32 lat_stride, u8* screen, u8* gbase, u32 lane, u32 env, u32 gid) {
+__device__ __noinline__ static void flush_lines(u32* lat, u32 lat_stride, u8* screen, u8* gbase, u32 il, u32 sh, u32 lane,
+                                                u32 env, u32 gid) {
     Mem m;
     m.g = gbase;
-    m.lane = lane;
+    m.lane = il;
+    m.sh = sh;
     u32* lat0 = lat;
     u32* lat1 = lat + lat_stride;
     u32* lat2 = lat + 2u * lat_stride;

@@ -109,4 +109,5 @@ struct PkRewardArgs {
     uint32_t max_steps;
     uint32_t reload_always;   // PK_F_RELOAD_ON_RESET
     uint32_t env0, env1;      // env range of this launch (sub-batches); arrays stay full-size [n]
+    uint32_t ilv_sh;          // image interleave (pk_layout.h pk_img_off)
 };

@@ -30,12 +30,18 @@ typedef uint8_t u8;
 namespace {
 
 struct RMem {
-    u8* g;          // group base
-    u32 lane;
+    u8* g;          // the env's image sub-block (pk_layout.h)
+    u32 lane, sh;   // lane within it, interleave shift
     const u32* regs;
     u32 np, env;
     u32 err;
 };
+
+__device__ __forceinline__ void rmem_at(RMem& M, u8* mem, u32 e, u32 sh) {
+    M.lane = e & (PK_LANES - 1u) & ((1u << sh) - 1u);
+    M.g = mem + pk_img_off(e, 0u, sh) - M.lane;
+    M.sh = sh;
+}
 
 __device__ __forceinline__ u32 bfe8(u32 v, u32 sh) { return (v >> sh) & 0xFFu; }
 
@@ -71,15 +77,15 @@ __device__ u32 rd(RMem& M, u32 a) {
                 default: return 0;
             }
         }
-        return M.g[(size_t)(a - 0xBE00u) * PK_LANES + M.lane];
+        return M.g[((size_t)(a - 0xBE00u) << M.sh) + M.lane];
     }
     if (a < 0xC000u) return 0;  // not reachable from the reward stack
-    return M.g[(size_t)(PK_P_WRAM + (a & 0x1FFFu)) * PK_LANES + M.lane];
+    return M.g[((size_t)(PK_P_WRAM + (a & 0x1FFFu)) << M.sh) + M.lane];
 }
 
 // PyBoy set_memory_value for WRAM (the only region the reward stack writes)
 __device__ __forceinline__ void wr(RMem& M, u32 a, u32 v) {
-    M.g[(size_t)(PK_P_WRAM + (a & 0x1FFFu)) * PK_LANES + M.lane] = (u8)v;
+    M.g[((size_t)(PK_P_WRAM + (a & 0x1FFFu)) << M.sh) + M.lane] = (u8)v;
 }
 
 __device__ __forceinline__ u32 rbit(RMem& M, u32 a, u32 b) { return (rd(M, a) >> b) & 1u; }
@@ -231,8 +237,7 @@ __global__ void __launch_bounds__(256) pk_reward_kernel(PkRewardArgs A) {
     u32* rs = A.rs;
     double* rsd = A.rsd;
     RMem M;
-    M.g = A.mem + (size_t)(e / PK_LANES) * PK_GROUP_STRIDE;
-    M.lane = e % PK_LANES;
+    rmem_at(M, A.mem, e, A.ilv_sh);
     M.regs = A.regs;
     M.np = np;
     M.env = e;
@@ -624,8 +629,7 @@ __global__ void __launch_bounds__(256) pk_rreset_pre_kernel(PkRewardArgs A) {
     u8 rl = 0;
     if (sel) {
         RMem M;
-        M.g = A.mem + (size_t)(e / PK_LANES) * PK_GROUP_STRIDE;
-        M.lane = e % PK_LANES;
+        rmem_at(M, A.mem, e, A.ilv_sh);
         M.regs = A.regs;
         M.np = A.npad;
         M.env = e;
@@ -644,8 +648,7 @@ __global__ void __launch_bounds__(256) pk_rreset_post_kernel(PkRewardArgs A) {
     const u32 np = A.npad;
     u32* rs = A.rs;
     RMem M;
-    M.g = A.mem + (size_t)(e / PK_LANES) * PK_GROUP_STRIDE;
-    M.lane = e % PK_LANES;
+    rmem_at(M, A.mem, e, A.ilv_sh);
     M.regs = A.regs;
     M.np = np;
     M.env = e;
@@ -696,9 +699,8 @@ __global__ void __launch_bounds__(256) pk_obs_kernel(PkRewardArgs A) {
         const u32 y = (u32)((t / (PK_OBS_W / 4u)) % PK_OBS_H);
         const u32 k = (u32)(t / ((size_t)PK_OBS_H * (PK_OBS_W / 4u)));
         const u32 e = A.oids ? A.oids[k] : A.env0 + k;
-        const u8* g = A.mem + (size_t)(e / PK_LANES) * PK_GROUP_STRIDE + (e % PK_LANES);
-        const int r = g[(size_t)(PK_P_WRAM + 0x1361u) * PK_LANES];
-        const int c = g[(size_t)(PK_P_WRAM + 0x1362u) * PK_LANES];
+        const int r = A.mem[pk_img_off(e, PK_P_WRAM + 0x1361u, A.ilv_sh)];
+        const int c = A.mem[pk_img_off(e, PK_P_WRAM + 0x1362u, A.ilv_sh)];
         const u8* srow = A.screen + (size_t)e * PK_SCREEN + (size_t)(2u * y) * PK_COLS + 8u * q;
         const uint2 sp = *reinterpret_cast<const uint2*>(srow);
         const u32* mk = A.mask + (size_t)e * PK_MASK_WORDS;
@@ -718,7 +720,8 @@ __global__ void __launch_bounds__(256) pk_obs_kernel(PkRewardArgs A) {
 }
 
 // bulk RAM gather/scatter for all envs: dense[e * len + i] <-> guest [addr, addr + len)
-__global__ void __launch_bounds__(256) pk_ram_copy_kernel(uint8_t* mem, uint8_t* dense, u32 n, u32 phys0, u32 len, u32 to_dense) {
+__global__ void __launch_bounds__(256) pk_ram_copy_kernel(uint8_t* mem, uint8_t* dense, u32 n, u32 sh, u32 phys0, u32 len,
+                                                          u32 to_dense) {
     const size_t total = (size_t)((n + PK_LANES - 1) / PK_LANES) * PK_LANES * len;
     for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
         // lane fastest: consecutive threads touch consecutive interleaved bytes
@@ -728,7 +731,7 @@ __global__ void __launch_bounds__(256) pk_ram_copy_kernel(uint8_t* mem, uint8_t*
         const u32 gid = (u32)(rest / len);
         const u32 e = gid * PK_LANES + lane;
         if (e >= n) continue;
-        uint8_t* p = mem + (size_t)gid * PK_GROUP_STRIDE + (size_t)(phys0 + i) * PK_LANES + lane;
+        uint8_t* p = mem + pk_img_off(e, phys0 + i, sh);
         if (to_dense) dense[(size_t)e * len + i] = *p;
         else *p = dense[(size_t)e * len + i];
     }
@@ -778,10 +781,10 @@ hipError_t pk_launch_obs(const PkRewardArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t pk_launch_ram_copy(uint8_t* mem, uint8_t* dense, u32 n, u32 phys0, u32 len, u32 to_dense, hipStream_t s) {
+hipError_t pk_launch_ram_copy(uint8_t* mem, uint8_t* dense, u32 n, u32 sh, u32 phys0, u32 len, u32 to_dense, hipStream_t s) {
     const u32 ngroups = (n + PK_LANES - 1) / PK_LANES;
     const size_t total = (size_t)ngroups * PK_LANES * len;
     const u32 grid = (u32)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
-    hipLaunchKernelGGL(pk_ram_copy_kernel, dim3(grid), dim3(256), 0, s, mem, dense, n, phys0, len, to_dense);
+    hipLaunchKernelGGL(pk_ram_copy_kernel, dim3(grid), dim3(256), 0, s, mem, dense, n, sh, phys0, len, to_dense);
     return hipGetLastError();
 }

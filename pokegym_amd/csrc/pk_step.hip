@@ -57,8 +57,13 @@
         st_acc[k] += (uint64_t)(t_ - st_prev);                  \
         st_prev = t_;                                           \
     } while (0)
+// the stage functions take the accumulators as extra arguments
+#define PK_STAMP_PARAMS , uint64_t* st_acc, uint64_t& st_prev
+#define PK_STAMP_ARGS , st_acc, st_prev
 #else
 #define PK_STAMP_AT(k) ((void)0)
+#define PK_STAMP_PARAMS
+#define PK_STAMP_ARGS
 #endif
 enum {
     PK_EV_EXEC = 1u << 0, PK_EV_F_LDS = 1u << 1, PK_EV_F_ROM16 = 1u << 2, PK_EV_F_BUS = 1u << 3,
@@ -119,13 +124,14 @@ struct St {
 // where this lane's emulator lives
 struct Ctx {
     const PkStepArgs* A;
-    u8* g;                // lane-interleaved RAM image of this wave's group
-    u32 lane, env, gid;
+    u8* g;                // this env's image sub-block (pk_layout.h: byte(phys) = g[phys << sh | lane])
+    u32 lane, sh;         // lane within the sub-block, interleave shift
+    u32 glane, env, gid;  // lane within the 64-env group (render latches), env, group
     u32 loc;              // env index within the workgroup (HRAM mirror column)
 };
 
-__device__ __forceinline__ u32 ld_img(const Ctx& c, u32 phys) { return c.g[phys * PK_LANES + c.lane]; }
-__device__ __forceinline__ void st_img(const Ctx& c, u32 phys, u32 v) { c.g[phys * PK_LANES + c.lane] = (u8)v; }
+__device__ __forceinline__ u32 ld_img(const Ctx& c, u32 phys) { return c.g[(phys << c.sh) + c.lane]; }
+__device__ __forceinline__ void st_img(const Ctx& c, u32 phys, u32 v) { c.g[(phys << c.sh) + c.lane] = (u8)v; }
 // keep the HRAM fetch mirror in step with a RAM write at guest address a (row PK_HC_ROWS = dummy)
 __device__ __forceinline__ void hcode_st(const Ctx& c, u32 a, u32 v) {
     const u32 row = sel(a - 0xFF80u < PK_HC_ROWS, a - 0xFF80u, PK_HC_ROWS);
@@ -311,7 +317,7 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
                 break;
             case 0xFF46: {  // OAM DMA: instantaneous 160-byte copy (pyboy mb.transfer_DMA)
                 if (s.npend) {
-                    flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.env, c.gid);
+                    flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.sh, c.glane, c.env, c.gid);
                     s.npend = 0;
                 }
                 const u32 src = v << 8;
@@ -347,7 +353,7 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
         return;
     }
     if (s.npend && vram_or_oam(a)) {
-        flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.env, c.gid);
+        flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.sh, c.glane, c.env, c.gid);
         s.npend = 0;
     }
     st_img(c, fast_phys(a), v);
@@ -357,14 +363,14 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
 // ---- rare paths (operate on a copy of the lane state) ----
 __device__ __forceinline__ u32 pk_fetch_slow(const PkStepArgs* A, u8* g, u32 lane, u32 loc, const St* sp, u32 pc) {
     Ctx c;
-    c.A = A; c.g = g; c.lane = lane; c.env = 0; c.gid = 0; c.loc = loc;
+    c.A = A; c.g = g; c.lane = lane; c.sh = A->ilv_sh; c.glane = 0; c.env = 0; c.gid = 0; c.loc = loc;
     const St s = *sp;
     return bus_read_any(c, s, pc) | (bus_read_any(c, s, (pc + 1u) & 0xFFFFu) << 8)
          | (bus_read_any(c, s, (pc + 2u) & 0xFFFFu) << 16);
 }
 __device__ __forceinline__ u32 pk_read_slow(const PkStepArgs* A, u8* g, u32 lane, u32 loc, const St* sp, u32 a0, u32 a1, u32 two) {
     Ctx c;
-    c.A = A; c.g = g; c.lane = lane; c.env = 0; c.gid = 0; c.loc = loc;
+    c.A = A; c.g = g; c.lane = lane; c.sh = A->ilv_sh; c.glane = 0; c.env = 0; c.gid = 0; c.loc = loc;
     const St s = *sp;
     const u32 m0 = bus_read_any(c, s, a0);
     const u32 m1 = two ? bus_read_any(c, s, a1) : 0u;
@@ -373,7 +379,7 @@ __device__ __forceinline__ u32 pk_read_slow(const PkStepArgs* A, u8* g, u32 lane
 __device__ __forceinline__ void pk_write_slow(const PkStepArgs* A, u8* g, u32 lane, u32 loc, u32 env, u32 gid, St* sp,
                                                   u32 a0, u32 v0, u32 a1, u32 v1, u32 two, u32 hifirst) {
     Ctx c;
-    c.A = A; c.g = g; c.lane = lane; c.env = env; c.gid = gid; c.loc = loc;
+    c.A = A; c.g = g; c.lane = lane; c.sh = A->ilv_sh; c.glane = env & (PK_LANES - 1u); c.env = env; c.gid = gid; c.loc = loc;
     St s = *sp;
     // a push writes SP-1 (high byte) before SP-2 (low byte), as PyBoy's push does
     if (two && hifirst) bus_write_any(c, s, a1, v1);
@@ -396,7 +402,7 @@ struct Ex {   // what the rest of the iteration needs from the instruction
     bool wr, wr2, wram;
 };
 template <bool PRIO>
-__device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, const Mc& m, u32& ev, Ex& x) {
+__device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, const Mc& m, u32& ev, Ex& x PK_STAMP_PARAMS) {
     const PkStepArgs& A = *c.A;
     const u32 D = m.D, U = m.U, K = m.K;
     // ---------------- operands, condition, memory address ----------------
@@ -416,8 +422,8 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
         // 512-byte block of plain RAM, where fast_phys is linear: o1 follows from o0.  A pair that
         // crosses a block boundary (incl. WRAM/echo at 0xE000 and echo/OAM at 0xFE00) is rare
         // and goes through the generic bus paths.
-        o0 = fast_phys(addr0) * PK_LANES + c.lane;
-        o1 = o0 + (u32)(sfield(D, PK_DB_ADIR, 2) * (int)PK_LANES);
+        o0 = (fast_phys(addr0) << c.sh) + c.lane;
+        o1 = o0 + ((u32)sfield(D, PK_DB_ADIR, 2) << c.sh);
         pair = ((addr0 ^ addr1) & 0xFE00u) == 0u;  // both in one 512-byte block
         // inside one 512-byte block both addresses share a region; only IO/IE can differ
         fast01 = ram_region(addr0) & pair & !io_addr(addr0) & !io_addr(addr1);
@@ -545,7 +551,7 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     x.o1 = o1;
 }
 
-__device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc& m, const Ex& x, u32& ev) {
+__device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc& m, const Ex& x, u32& ev PK_STAMP_PARAMS) {
     const PkStepArgs& A = *c.A;
     if (x.wram) {
         // VRAM / OAM change while rendered lines are pending: rasterise them first (rare)
@@ -554,7 +560,7 @@ __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc&
             PK_STAMP_AT(2);
             if (vram_or_oam(x.addr0) | (x.wr2 & vram_or_oam(x.addr1))) {
                 PK_STAMP_AT(11);
-                flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, env, c.gid);
+                flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.sh, c.glane, env, c.gid);
                 PK_STAMP_AT(10);
                 s.npend = 0;
                 ev |= PK_EV_FLUSH;
@@ -611,10 +617,14 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
     if (env >= ((A.env1 + PK_LANES - 1u) & ~(PK_LANES - 1u))) return;
     Ctx c;
     c.A = &A;
-    c.lane = env & (PK_LANES - 1u);
+    c.glane = env & (PK_LANES - 1u);
     c.env = env;
     c.gid = __builtin_amdgcn_readfirstlane(env / PK_LANES);
-    c.g = A.mem + (size_t)c.gid * PK_GROUP_STRIDE;
+    // image sub-block of this env (interleave 1 << ilv_sh >= the wave's envs: one per wave)
+    c.sh = A.ilv_sh;
+    c.lane = c.glane & ((1u << c.sh) - 1u);
+    c.g = A.mem + (size_t)c.gid * PK_GROUP_STRIDE
+        + (((size_t)__builtin_amdgcn_readfirstlane(c.glane >> c.sh) * PK_PHYS) << c.sh);
     c.loc = (threadIdx.x >> 6) * A.wave_lanes + wl;  // < PK_WG_ENVS envs per workgroup
     for (u32 i = 0; i < PK_HC_ROWS; i++) lds_rom[PK_HC_BASE + c.loc * PK_HC_STRIDE + i] = (u8)ld_img(c, PK_P_HRAM + i);
 
@@ -751,7 +761,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         const uint4 u2 = ucv2[2u * i2], u2b = ucv2[2u * i2 + 1u];
         // ---------------- execute ----------------
         Ex x;
-        pk_exec<PRIO>(s, c, pc, bytes, m, ev, x);
+        pk_exec<PRIO>(s, c, pc, bytes, m, ev, x PK_STAMP_ARGS);
         u32 cycles = x.cycles;
         const bool wr = x.wr, wram = x.wram;
         // ---------------- fused secondary op (pk_ucode.h pk_u2_entry) ----------------
@@ -832,7 +842,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         }
 
         // ---------------- memory writes (wv0 at addr0, wv1 at addr1) ----------------
-        pk_write(s, c, env, m, x, ev);
+        pk_write(s, c, env, m, x, ev PK_STAMP_ARGS);
 
         // ---------------- prefetch the next instruction (LDS-staged ROM or the HRAM mirror) ----------------
         // wave priority (two waves per SIMD): from here through the next iteration's fetch, decode
@@ -904,7 +914,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
                         const u32 y0 = sel(nm == 2u, ly + 1u, ly);   // nm 2: this line's mode-0 event has passed
                         for (u32 y = y0; y < PK_ROWS; y++) {
                             if (wline && wy <= y) lw += 1;
-                            const u32 idx = (c.gid * PK_ROWS + y) * PK_LANES + c.lane;
+                            const u32 idx = (c.gid * PK_ROWS + y) * PK_LANES + c.glane;
                             A.lat[idx] = l0;
                             A.lat[A.lat_stride + idx] = l1;
                             A.lat[2u * A.lat_stride + idx] = (u32)(lw + 1) | 0x100u;
@@ -984,7 +994,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
                     const u32 wy = bfe8(s.lcd1, 16), wx = bfe8(s.lcd1, 24);
                     int lw = (int)bfe8(s.misc, 16) - 1;
                     if ((lcdc & 0x20u) && wy <= ly && (int)wx - 7 < (int)PK_COLS) lw += 1;
-                    const u32 idx = (c.gid * PK_ROWS + ly) * PK_LANES + c.lane;
+                    const u32 idx = (c.gid * PK_ROWS + ly) * PK_LANES + c.glane;
                     A.lat[idx] = lcdc | (bfe8(s.lcd1, 8) << 8) | (bfe8(s.lcd1, 0) << 16) | (wx << 24);
                     A.lat[A.lat_stride + idx] = wy | ((s.lcd2 & 0xFFFFFFu) << 8);
                     A.lat[2u * A.lat_stride + idx] = (u32)(lw + 1) | 0x100u;

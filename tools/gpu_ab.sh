@@ -1,6 +1,8 @@
 #!/bin/bash
-# A/B/n bench: each pokegym_amd/lib/libpokegym_amd_<name>.so in $LIBS on each workload in $WLS,
-# interleaved (ABAB) to spread clock drift; parity of the first library's kernels when $PARITY is set.
+# A/B/n bench: each variant in $LIBS on each workload in $WLS, interleaved (ABAB) to spread clock
+# drift; parity of the first variant's kernels when $PARITY is set.  A variant is a library name
+# (pokegym_amd/lib/libpokegym_amd_<name>.so) optionally followed by @VAR=value (an environment
+# setting for that run, e.g. "ilv@PK_ILV=64"; the output files use the part before '@' plus the value).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
@@ -8,14 +10,20 @@ O=$R/gpurun_out/ab_${1:-x}
 mkdir -p $O
 STEPS=${STEPS:-8}
 rc=0
+runenv() {  # variant -> "PK_LIB=... [VAR=value]"
+  local n=${1%%@*} e=""
+  [[ $1 == *@* ]] && e=${1#*@}
+  echo "PK_LIB=$R/pokegym_amd/lib/libpokegym_amd_$n.so $e"
+}
+tag() { local t=${1//@/_}; echo ${t//=/}; }
 if [ -n "$PARITY" ]; then
   n=${LIBS%% *}
-  env PK_LIB=$R/pokegym_amd/lib/libpokegym_amd_$n.so timeout -k 10 600 python -u -m pytest ${PARITY_FILES:-tests/test_gpu_parity.py} -x -q --timeout 200 --timeout-method thread -k "$PARITY" > $O/par_$n.log 2>&1 || { rc=$?; echo "exit=$rc" > $O/exit.txt; exit $rc; }
+  env $(runenv $n) timeout -k 10 600 python -u -m pytest ${PARITY_FILES:-tests/test_gpu_parity.py} -x -q --timeout 200 --timeout-method thread -k "$PARITY" > $O/par_$(tag $n).log 2>&1 || { rc=$?; echo "exit=$rc" > $O/exit.txt; exit $rc; }
 fi
 for rep in 1 2; do
   for w in $WLS; do
     for n in $LIBS; do
-      env PK_LIB=$R/pokegym_amd/lib/libpokegym_amd_$n.so timeout -k 10 300 python bench.py --steps $STEPS --warmup 2 --no-cpu-baseline --workload $w $BENCH_EXTRA > $O/${w}_${n}_$rep.json 2>> $O/err.log || { rc=$?; break 3; }
+      env $(runenv $n) timeout -k 10 300 python bench.py --steps $STEPS --warmup 2 --no-cpu-baseline --workload $w $BENCH_EXTRA > $O/${w}_$(tag $n)_$rep.json 2>> $O/err.log || { rc=$?; break 3; }
     done
   done
 done
