@@ -113,7 +113,7 @@ def _cpu_baseline(rom: bytes, state, seconds_target: float = 10.0):
     v72, wall72, ips72 = _cpu_run(rom, state, 72, 1, steps72, 2000)
     steps_s = max(4, int(seconds_target / 4 / per_step))
     vs, walls, _ = _cpu_run(rom, state, share, 4, steps_s, 1000)
-    inten = oracle.intensity(rom, state, 8, 3, 4, 99)
+    inten = oracle.intensity(rom, state, 32, 3, 8, 99)   # 256 env-steps of the same action stream
     return {
         "value": round(v72, 1),
         "unit": "env-steps/s",
