@@ -420,17 +420,20 @@ def main():
                              "diagnostic, not the default line)") if args.host_obs else None,
                 "scaling_note": ("the default workload is configs[2] (config3: 65,536 envs on one GPU) at N=1 and "
                                  "configs[3] itself (config4: 262,144 envs split over the N GPUs, strong scaling) at "
-                                 "N>1.  A GPU's rate depends on its env count — 32,768 envs: ~305k env-steps/s, "
-                                 "65,536: ~490k, 131,072: ~720k (one launch needs 64 envs per SIMD to hide its "
-                                 "latency and 128 to fill every lane; profiles/r02r/envs) — so N=8 "
-                                 "(32,768 per GPU) is below 8x the N=1 rate by construction of configs[3]"),
+                                 "N>1.  A GPU's rate depends on its env count (config4 through VecEnv, round 3: "
+                                 "32,768 envs ~287k env-steps/s, 65,536 ~433k, 131,072 ~662k, 262,144 ~940k; "
+                                 "profiles/r03) — one launch needs 64 envs per SIMD to hide K1's latency and 128 to "
+                                 "fill every lane — so N=8 (32,768 per GPU) is below 8x the N=1 rate by construction "
+                                 "of configs[3]"),
             },
             "roofline": {
                 "bound": "hbm",
-                "measured_bound": ("issue + dependent latency (not HBM, not MFMA): per emulated SM83 instruction a wave "
-                                   "issues the fetch -> decode -> address -> operand-read chain and a ~100-instruction "
-                                   "VALU datapath; `issue` below carries the PMC figures and `frac` is only the HBM "
-                                   "price of the algorithmic bytes (DESIGN.md section 5)"),
+                "measured_bound": ("dependent latency + issue (not HBM, not MFMA): per loop iteration (one emulated "
+                                   "SM83 instruction, two when a register-only successor fuses) a wave runs the LDS "
+                                   "fetch -> microcode -> address -> operand-read chain of its divergent lanes and the "
+                                   "fused datapath; with two waves per SIMD the chain dominates, with one converged "
+                                   "wave (config2) issue does.  `issue` carries the PMC ISA counts per emulated "
+                                   "instruction; `frac` is only the HBM price of the algorithmic bytes (DESIGN.md §5)"),
                 "kernel": ("pk_step_kernel (K1, 24 emulated frames) + pk_render_kernel (K2)"
                            + (" + pk_reward_kernel/pk_obs_kernel (K4/K3)" if reward else "")),
                 "span": ("sum of the step's kernel times per launch (HIP events on the launch stream, averaged "
@@ -441,9 +444,13 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
-                "traffic": (stamp or {}).get("hbm_bytes_per_launch_k1"),
+                # per launch of THIS run: the profiled per-env-step bytes x the envs one launch covers
+                "traffic": (round(stamp["hbm_bytes_per_env_step_k1"] * envs_per_launch) if stamp and
+                            "hbm_bytes_per_env_step_k1" in stamp else (stamp or {}).get("hbm_bytes_per_launch_k1")),
+                "traffic_per_env_step": (stamp or {}).get("hbm_bytes_per_env_step_k1"),
                 "traffic_source": (f"{stamp_src}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this "
-                                   "workload (not measured inside this run)") if stamp else None,
+                                   "workload (K1 only; L2 memory-side requests, Infinity-Cache hits included; "
+                                   "not measured inside this run)") if stamp else None,
                 "bytes_per_env_step": B,
                 "span_ms": round(span_s * 1e3, 3),
                 "k1_ms": round(k1_s * 1e3, 3),

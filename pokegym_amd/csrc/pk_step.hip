@@ -873,6 +873,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
             pf = sel(fl | fh | fg, 1u, 0u);
         }
 
+
         // ---------------- HALT fast-forward, timer, LCD (pyboy mb.tick) ----------------
         // Common case: a running CPU whose cycles reach neither the next LCD event (nor, LCD off,
         // the frame length), with the timer off and the watchdog budget left — then the whole stage

@@ -53,6 +53,8 @@ def main():
             if "pk_step_kernel" in row["Name"]:
                 k1.append(float(row["AverageNs"]) / 1e6)
     bench = json.loads(open(os.path.join(D, "stats_bench.json")).read().strip().splitlines()[-1])
+    # envs one K1 dispatch covers (a VecEnv sub-batch, or the whole shard)
+    epl = bench["config"].get("vecenv_batch_size") or bench["config"]["envs_per_gpu"]
     # issue: ISA instructions a wave issues per emulated SM83 instruction of one of its envs
     # (SQ_INSTS_* / SQ_WAVES / the instructions one env executes in the launch)
     issue = None
@@ -79,6 +81,10 @@ def main():
         "calibration": {"FETCH_SIZE_per_GiB": cf, "WRITE_SIZE_per_GiB": cw},
         "k1_read_bytes": int(rd), "k1_write_bytes": int(wr),
         "hbm_bytes_per_launch_k1": int(rd + wr),
+        "envs_per_launch": epl,
+        "hbm_bytes_per_env_step_k1": round((rd + wr) / epl, 1),
+        "traffic_level": "FETCH_SIZE / WRITE_SIZE = the L2's memory-side (fabric) requests (TCC_EA0_RDREQ / _WRREQ): "
+                         "L2 misses, served by the Infinity Cache (MALL) or HBM — MALL hits are counted",
         "valu_busy_pct": round(busy, 2),
         "valu_busy_formula": "100*sum(SQ_ACTIVE_INST_VALU)/CU_NUM/max(GRBM_GUI_ACTIVE) (rocprofv3 VALUBusy, gfx94x form)",
         "valu_utilization_pct": round(util, 2),
