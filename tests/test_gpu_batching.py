@@ -113,3 +113,39 @@ def test_vecenv_padded_slots_step_and_savestates():
     assert sub.save_state(50) == st
     full.close()
     sub.close()
+
+
+def test_vecenv_sub_batches_log_raises_injected_error():
+    """VecEnv(256, batch_size=64) through recv/send with a logging interval: an error
+    code a sub-batch step writes on its own stream is not lost to the logging interval's check and
+    clear — the reference's exception (KeyError: MAP_ID_REF lookup of an unknown map id,
+    environment.py:739) is raised at the first interval after the step that hit it, and the
+    episode statistics of every sub-batch are all-reduced in each interval."""
+    import torch
+    from pokegym_amd.env import VecEnv
+    from pokegym_amd.testrom.game import game_rom
+    n, bs, log = 256, 64, 4
+    v = VecEnv(n, rom=game_rom(), power_on=True, batch_size=bs, max_episode_steps=3, log_interval=log)
+    g = torch.Generator(device=v.device)
+    g.manual_seed(7)
+    v.async_reset()
+    bad_env, raised, infos_seen, sends = 70, None, [], 0
+    for rnd in range(3 * log):
+        for b in range(n // bs):
+            o, r, d, t, infos, ids, m = v.recv()
+            infos_seen += infos
+            if rnd == log + 1 and int(ids[0]) == 64:          # env 70 is in the second sub-batch
+                torch.cuda.synchronize()
+                v.emu.poke(v.phys(bad_env), 0xD35E, bytes([0xF8]))   # map id 248: not in MAP_ID_REF
+            try:
+                v.send(torch.randint(0, 8, (bs,), device=v.device, generator=g).to(torch.uint8))
+                sends += 1
+            except KeyError as e:
+                raised = (rnd, str(e))
+                break
+        if raised:
+            break
+    v.close()
+    assert raised is not None and f"env {bad_env}" in raised[1], raised
+    assert raised[0] <= 2 * log + 1, raised            # at the first interval after the poke
+    assert infos_seen and all(i["episodes"] > 0 for i in infos_seen)
