@@ -407,9 +407,9 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     ALLOC(h->t_screen, PK_SCREEN);
     ALLOC(h->scratch, PK_PHYS + PK_NREGS * 4 + 3 * PK_ROWS * 4 + PK_SCREEN);
     ALLOC(h->lists, (2 * (size_t)h->ngroups + 2 * (size_t)h->npad) * 4);
-#ifdef PK_STAMP
-    ALLOC(h->dbg, 64 * 8);
-    (void)hipMemset(h->dbg, 0, 64 * 8);
+#if defined(PK_STAMP) || defined(PK_WAVETIME)
+    ALLOC(h->dbg, PK_DBG_WORDS * 8);
+    (void)hipMemset(h->dbg, 0, PK_DBG_WORDS * 8);
 #endif
     if (h->flags & PK_F_REWARD) {
         ALLOC(h->rs, (size_t)RS_NFIELDS * h->npad * 4);
@@ -931,8 +931,8 @@ int pk_debug_counters(pk_handle* h, uint64_t* out, uint32_t n) {
     if (!h->dbg) return 0;
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpy(out, h->dbg, (size_t)(n < 64 ? n : 64) * 8, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemset(h->dbg, 0, 64 * 8));
+    HIPCHK(hipMemcpy(out, h->dbg, (size_t)(n < PK_DBG_WORDS ? n : PK_DBG_WORDS) * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemset(h->dbg, 0, PK_DBG_WORDS * 8));
     return 0;
 }
 

@@ -72,6 +72,13 @@ enum {
 };
 
 // largest K1 workgroup (one per CU: its envs share one LDS copy of the ROM banks and microcode):
+// diagnostic buffer (-DPK_STAMP phase counters; -DPK_WAVETIME adds one PK_WT_REC-word record per K1 wave)
+#ifdef PK_WAVETIME
+#define PK_WT_REC 6u
+#define PK_DBG_WORDS (64u + PK_WT_REC * 16384u)
+#else
+#define PK_DBG_WORDS 64u
+#endif
 // 512 threads = 8 waves, two per SIMD at 221 VGPRs; at most PK_WG_ENVS envs (HRAM code mirror columns)
 #ifndef PK_K1_MAX_THREADS
 #define PK_K1_MAX_THREADS 512

@@ -627,6 +627,12 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         + (((size_t)__builtin_amdgcn_readfirstlane(c.glane >> c.sh) * PK_PHYS) << c.sh);
     c.loc = (threadIdx.x >> 6) * A.wave_lanes + wl;  // < PK_WG_ENVS envs per workgroup
     for (u32 i = 0; i < PK_HC_ROWS; i++) lds_rom[PK_HC_BASE + c.loc * PK_HC_STRIDE + i] = (u8)ld_img(c, PK_P_HRAM + i);
+#ifdef PK_WAVETIME
+    // diagnostic build (tools/wavetime_run.py): per-wave start/end (s_memrealtime, 100 MHz), loop
+    // iterations of lane 0, hardware slot, and the wave's largest per-lane instruction count
+    const uint64_t wt0 = __builtin_amdgcn_s_memrealtime();
+    u32 wt_iter = 0;
+#endif
 
     const u32 np = A.npad;
     u32* R = A.regs;
@@ -682,6 +688,9 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
 #endif
     while (frame < A.frames) {
         u32 ev = 0;
+#ifdef PK_WAVETIME
+        wt_iter++;
+#endif
         PK_STAMP_AT(8);
 #ifdef PK_STAMP
         st_iter++;
@@ -1035,6 +1044,23 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         for (int k = 0; k < PK_NSTAMP; k++) atomicAdd(&A.dbg[k], (unsigned long long)st_acc[k]);
         atomicAdd(&A.dbg[PK_NSTAMP], (unsigned long long)st_iter);
         atomicAdd(&A.dbg[PK_NSTAMP + 1], 1ull);
+    }
+#endif
+#ifdef PK_WAVETIME
+    {
+        const uint64_t wt1 = __builtin_amdgcn_s_memrealtime();
+        const u32 w = tid >> 6;
+        unsigned long long* rec = A.dbg + 64u + PK_WT_REC * (size_t)w;
+        if (A.dbg && w < 16384u) {
+            if (wl == 0u) {
+                rec[0] = wt0;
+                rec[1] = wt1;
+                rec[2] = wt_iter;
+                rec[3] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));    // HW_ID
+                rec[4] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11));   // XCC_ID
+            }
+            atomicMax(&rec[5], (unsigned long long)icount);
+        }
     }
 #endif
     if (!active) return;
