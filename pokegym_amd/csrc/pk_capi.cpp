@@ -359,9 +359,9 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
         uint32_t ilv = k1_wave_lanes(h, h->n);
         if (const char* iv = getenv("PK_ILV")) {
             int v = atoi(iv);
-            if (v < 1 || v > 64 || (v & (v - 1)) || (uint32_t)v < ilv) {
+            if (v < 1 || v > 64 || (v & (v - 1))) {
                 delete h;
-                return fail(-EINVAL, "PK_ILV must be a power of two <= 64 and >= K1's envs per wave (%u)", ilv);
+                return fail(-EINVAL, "PK_ILV must be a power of two <= 64");
             }
             ilv = (uint32_t)v;
         }

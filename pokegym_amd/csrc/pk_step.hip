@@ -389,6 +389,79 @@ __device__ __forceinline__ void pk_write_slow(const PkStepArgs* A, u8* g, u32 la
 }
 
 // ---------------------------------------------------------------------------------------------
+// Block copy.  pokered's CopyData (home/copy.asm: copy BC bytes from HL to DE) and the same loop
+// with B and C swapped in the zero test,
+//     ld a,[hli] / ld [de],a / inc de / dec bc / ld a,c (ld a,b) / or b (or c) / jr nz,-8
+// is the bulk of a map load with the LCD off (tileset graphics into VRAM).  K1 runs it one
+// instruction (or two, fused) per loop iteration, 7 instructions per byte; here up to PK_COPY_CAP
+// whole passes run at the top of one iteration — their bytes copied in batches; registers, flags,
+// cycles, watchdog budget and instruction count set as the 7k instructions set them — and the
+// iteration goes on to execute the next pass's first instruction (pc is unchanged: at least one
+// pass is left).  Only when nothing can happen inside the passes: CPU running with no interrupt
+// pending, timer off, their cycles (and the next instruction's) below the next LCD event (LCD off:
+// the frame end) and inside the watchdog budget; code in staged ROM; source in staged ROM, VRAM
+// or WRAM, destination in VRAM or WRAM (no echo, OAM, HRAM or IO), disjoint; no rendered lines
+// pending.  Returns the passes' cycles (0: not taken).
+#define PK_COPY_W0 0x0B13122Au          // 2A 12 13 0B: ld a,[hli] / ld [de],a / inc de / dec bc
+#define PK_COPY_W1A 0xF820B079u         // 79 B0 20 F8: ld a,c / or b / jr nz,-8 (pokered)
+#define PK_COPY_W1B 0xF820B178u         // 78 B1 20 F8: ld a,b / or c / jr nz,-8
+#define PK_COPY_CAP 64u
+__device__ __forceinline__ bool copy_ram(u32 a) { return (a - 0x8000u < 0x2000u) | (a - 0xC000u < 0x2000u); }
+__device__ __forceinline__ u32 pk_copy_loop(St& s, const Ctx& c, u32 pc, int& slack, u32& icount) {
+    const u32 cpu = s.cpu;
+    if ((cpu & (CPU_CRASH | CPU_HALT | CPU_QUEUED)) | ((cpu >> 8) & (cpu >> 16) & 0x1Fu)) return 0;
+    if (s.npend | (s.tim0 & (4u << 24))) return 0;
+    if (!rom_staged(s, pc) || (pc & 0x3FFFu) > 0x3FF8u) return 0;
+    const u32 li = rom_lds_index(s, pc) + 4u;
+    const u32* romw = reinterpret_cast<const u32*>(lds_rom);
+    const u32 w1 = __builtin_amdgcn_alignbyte(romw[(li >> 2) + 1u], romw[li >> 2], li & 3u);
+    if (w1 != PK_COPY_W1A && w1 != PK_COPY_W1B) return 0;
+    const u32 bc = s.w0 & 0xFFFFu, de = s.w0 >> 16, hl = s.w1 & 0xFFFFu;
+    u32 k = (bc == 0u ? 0x10000u : bc) - 1u;          // passes before the last one
+    k = min(k, PK_COPY_CAP);
+    // 52 cycles and 59 watchdog units per pass; the iteration's own ld a,[hli]: 8 and 9
+    const u32 lim = sel(s.lcd0 & 0x80u, s.target, FRAME_CYCLES);
+    if (lim < s.clock + 9u || slack < 9) return 0;
+    k = min(k, (lim - s.clock - 9u) / 52u);
+    k = min(k, (u32)(slack - 9) / 59u);
+    // destination: inside one VRAM or WRAM region
+    if (!copy_ram(de)) return 0;
+    k = min(k, ((de | 0x1FFFu) + 1u) - de);
+    // source: staged ROM (inside its bank) or VRAM / WRAM (inside its region, disjoint from the
+    // destination)
+    const bool srom = hl < 0x8000u;
+    if (srom) {
+        if (!rom_staged(s, hl)) return 0;
+        k = min(k, ((hl | 0x3FFFu) + 1u) - hl);
+    } else {
+        if (!copy_ram(hl)) return 0;
+        k = min(k, ((hl | 0x1FFFu) + 1u) - hl);
+        k = min(k, hl > de ? hl - de : de - hl);
+    }
+    if (k == 0u) return 0;
+    const u32 sb = srom ? rom_lds_index(s, hl) : fast_phys(hl);
+    const u32 db = fast_phys(de);
+    for (u32 i0 = 0; i0 < k; i0 += 16u) {
+        u32 b[16];
+#pragma unroll
+        for (u32 j = 0; j < 16u; j++) {
+            const u32 i = min(i0 + j, k - 1u);
+            b[j] = srom ? (u32)lds_rom[sb + i] : ld_img(c, sb + i);
+        }
+#pragma unroll
+        for (u32 j = 0; j < 16u; j++)
+            if (i0 + j < k) st_img(c, db + i0 + j, b[j]);
+    }
+    const u32 nbc = (bc - k) & 0xFFFFu;                // >= 1: the loop goes on
+    const u32 a = (nbc >> 8) | (nbc & 0xFFu);
+    s.w0 = nbc | (((de + k) & 0xFFFFu) << 16);
+    s.w1 = ((hl + k) & 0xFFFFu) | (sel(a == 0u, 0x80u, 0u) << 16) | (a << 24);
+    slack -= (int)(7u * k);                            // the tail subtracts the cycles
+    icount += 7u * k;
+    return 52u * k;
+}
+
+// ---------------------------------------------------------------------------------------------
 // One emulated instruction's execution: address, operand reads, fused datapath, control
 // (pk_exec) and memory writes (pk_write), the same straight-line all-units sequence in every lane.
 // (A wave-uniform variant — scalar branches around the units an instruction does not use when
@@ -622,9 +695,13 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
     c.gid = __builtin_amdgcn_readfirstlane(env / PK_LANES);
     // image sub-block of this env (interleave 1 << ilv_sh >= the wave's envs: one per wave)
     c.sh = A.ilv_sh;
-    c.lane = c.glane & ((1u << c.sh) - 1u);
-    c.g = A.mem + (size_t)c.gid * PK_GROUP_STRIDE
-        + (((size_t)__builtin_amdgcn_readfirstlane(c.glane >> c.sh) * PK_PHYS) << c.sh);
+    // c.g is wave-uniform (the sub-block of the wave's first env); an interleave narrower than the
+    // wave puts the wave's envs in several sub-blocks, reached through the per-lane offset
+    {
+        const u32 sub = c.glane >> c.sh, sub0 = __builtin_amdgcn_readfirstlane(sub);
+        c.g = A.mem + (size_t)c.gid * PK_GROUP_STRIDE + (((size_t)sub0 * PK_PHYS) << c.sh);
+        c.lane = (((sub - sub0) * PK_PHYS) << c.sh) + (c.glane & ((1u << c.sh) - 1u));
+    }
     c.loc = (threadIdx.x >> 6) * A.wave_lanes + wl;  // < PK_WG_ENVS envs per workgroup
     for (u32 i = 0; i < PK_HC_ROWS; i++) lds_rom[PK_HC_BASE + c.loc * PK_HC_STRIDE + i] = (u8)ld_img(c, PK_P_HRAM + i);
 #ifdef PK_WAVETIME
@@ -762,6 +839,11 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         ev |= sel(exec, PK_EV_EXEC | sel((bytes & 0xFFu) == 0xCBu, PK_EV_CB, 0u), 0u) | sel(pf != 0u, PK_EV_F_LDS, 0u)
             | sel(dispatch, PK_EV_INT, 0u) | sel(!exec && !dispatch, PK_EV_IDLE, 0u);
         if (exec) PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, bytes & 0xFFu);
+        // ---------------- block copy: the CopyData loop (pk_copy_loop) ----------------
+        // whole passes of the loop run here; the iteration then executes the next pass's first
+        // instruction as usual (the loop's first bytes identify it: no INT pseudo-op has them)
+        u32 bcyc = 0;
+        if (PK_RARE(bytes == PK_COPY_W0)) bcyc = pk_copy_loop(s, c, pc, slack, icount);
         const Mc m = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y, e2.z, e2.w, e3.x, e3.y, e3.z, e3.w};
         const u32 D = m.D;
         // the successor's secondary-op entry (read now: its LDS latency overlaps the execute stage)
@@ -771,7 +853,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         // ---------------- execute ----------------
         Ex x;
         pk_exec<PRIO>(s, c, pc, bytes, m, ev, x PK_STAMP_ARGS);
-        u32 cycles = x.cycles;
+        u32 cycles = x.cycles + bcyc;
         const bool wr = x.wr, wram = x.wram;
         // ---------------- fused secondary op (pk_ucode.h pk_u2_entry) ----------------
         // The instruction after this one, if it is a JR (cc), LD r,r', INC/DEC r, INC/DEC BC/DE/HL or

@@ -246,3 +246,64 @@ def hram_code_rom() -> bytes:
           "jp main",
           "r_loop:", f"db {loop}", "r_imm:", f"db {imm}"]
     return build_rom("\n".join(L), n_banks=2, title="HRAMCODE")
+
+
+def copydata_rom() -> bytes:
+    """pokered's CopyData loop (home/copy.asm) and its B/C-swapped twin — which K1 runs in blocks of
+    whole passes (pk_step.hip pk_copy_loop) — called with per-env parameters from the joypad and an
+    LFSR: sources in ROM bank 0, the switchable bank, WRAM and VRAM; destinations in VRAM and WRAM,
+    overlapping the source either way, and — where the block path must step aside — HRAM and OAM;
+    lengths 1..512; the LCD on with the VBlank, STAT (HBlank, some passes) and timer interrupts
+    enabled, so interrupts land inside copies; the timer switched on and off; every 16th pass a
+    1 KiB ROM-to-VRAM copy with the LCD off (pokered's DisableLCD regime)."""
+    L = ["wSeed equ $c0f0", "wPass equ $c0f1", "wVbl equ $c0f2", "wStat equ $c0f3", "wR0 equ $c0f4", "wR1 equ $c0f5",
+         "section 0",
+         "org $0040", "jp h_vbl", "org $0048", "jp h_stat", "org $0050", "reti", "org $0058", "reti", "org $0060", "reti",
+         "org $0100", "nop", "jp start", "org $0150",
+         "start:", "di", "ld sp, $dff0",
+         "ld a, 1", "ld [$2000], a",                          # MBC3: bank 1 switchable
+         "ld a, $5a", "ld [wSeed], a", "xor a", "ld [wPass], a",
+         "ld a, $07", "ldh [$ff], a",                         # IE: VBlank, STAT, timer
+         "ld a, $e3", "ldh [$40], a", "ei",
+         "main:",
+         # two LFSR bytes, the joypad mixed in
+         "ld a, $20", "ldh [$00], a", "ldh a, [$00]", "ldh a, [$00]", "ld b, a",
+         "ld a, [wSeed]", "xor b", "add a, a", "jr nc, .n1", "xor $1d", ".n1:", "ld [wR0], a",
+         "add a, a", "jr nc, .n2", "xor $1d", ".n2:", "ld [wR1], a", "ld [wSeed], a",
+         "ld a, [wPass]", "inc a", "ld [wPass], a", "ld d, a",
+         # every 8th pass: the timer on or off (TAC 5 / 0); STAT HBlank interrupt on some passes
+         "and $07", "jr nz, .t1", "ld a, d", "and $08", "rrca", "or $01", "and $05", "ldh [$07], a", ".t1:",
+         "ld a, [wR1]", "and $08", "ldh [$41], a",
+         # every 16th pass: 1 KiB ROM -> VRAM with the LCD off
+         "ld a, d", "and $0f", "jr nz, .nolcd",
+         "xor a", "ldh [$0f], a", "ldh a, [$ff]", "push af", "res 0, a", "ldh [$ff], a",
+         ".wly:", "ldh a, [$44]", "cp 145", "jr nz, .wly",
+         "ldh a, [$40]", "and $7f", "ldh [$40], a",
+         "ld hl, $0000", "ld de, $8800", "ld bc, $0400", "call copy_a",
+         "ldh a, [$40]", "or $80", "ldh [$40], a", "xor a", "ldh [$0f], a", "pop af", "ldh [$ff], a",
+         ".nolcd:",
+         # length: BC = 1..512
+         "ld a, [wR0]", "and $01", "ld b, a", "ld a, [wR1]", "ld c, a", "or b", "jr nz, .len", "inc c", ".len:",
+         # source (wR0 bits 7-6): ROM bank 0 / bank 1 / WRAM / VRAM, + 8 * (wR1 & $3f)
+         "ld a, [wR1]", "and $3f", "ld l, a", "ld h, 0", "add hl, hl", "add hl, hl", "add hl, hl",
+         "ld a, [wR0]", "and $c0", "jr nz, .s1", "ld a, $02", "jr .sh", ".s1:",
+         "cp $40", "jr nz, .s2", "ld a, $40", "jr .sh", ".s2:",
+         "cp $80", "jr nz, .s3", "ld a, $c4", "jr .sh", ".s3:", "ld a, $80", ".sh:",
+         "add a, h", "ld h, a",
+         # destination (wR0 bits 5-3)
+         "ld a, [wR0]", "and $38", "rrca", "rrca", "rrca", "ld e, a",
+         "cp 2", "jr nc, .d2", "ld d, $90", "jr .dlow", ".d2:",
+         "cp 4", "jr nc, .d4", "ld d, $d0", "jr .dlow", ".d4:",
+         "cp 5", "jr nc, .d5", "ld a, l", "add a, 5", "ld e, a", "ld a, h", "adc a, 0", "ld d, a", "jr .dgo", ".d5:",
+         "cp 6", "jr nc, .d6", "ld a, l", "sub 7", "ld e, a", "ld a, h", "sbc a, 0", "ld d, a", "jr .dgo", ".d6:",
+         # HRAM / OAM: short copies only
+         "ld b, 0", "ld a, c", "and $1f", "inc a", "ld c, a",
+         "ld a, e", "cp 6", "jr nz, .d7", "ld de, $ff90", "jr .dgo", ".d7:", "ld de, $fe10", "jr .dgo",
+         ".dlow:", "ld a, [wR1]", "and $3f", "rlca", "rlca", "ld e, a",
+         ".dgo:",
+         "ld a, [wR1]", "and $01", "jr nz, .vb", "call copy_a", "jp main", ".vb:", "call copy_b", "jp main",
+         "h_vbl:", "push af", "ld a, [wVbl]", "inc a", "ld [wVbl], a", "pop af", "reti",
+         "h_stat:", "push af", "ld a, [wStat]", "inc a", "ld [wStat], a", "pop af", "reti",
+         "copy_a:", "ld a, [hl+]", "ld [de], a", "inc de", "dec bc", "ld a, c", "or b", "jr nz, copy_a", "ret",
+         "copy_b:", "ld a, [hl+]", "ld [de], a", "inc de", "dec bc", "ld a, b", "or c", "jr nz, copy_b", "ret"]
+    return build_rom("\n".join(L), n_banks=2, title="COPYDATA")

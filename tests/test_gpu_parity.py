@@ -192,3 +192,20 @@ def test_map_load_warp_parity(shape, monkeypatch):
     ref, _ = oracle.batch_run(rom, state, acts, want_screens=False)
     bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
     assert not bad, bad[:4]
+
+
+@pytest.mark.parametrize("shape", [("", ""), ("16", "512"), ("32", "512")])
+def test_copydata_block_path_parity(shape, monkeypatch):
+    """pokered's CopyData loop and its B/C twin, which K1 runs in blocks of whole passes
+    (pk_step.hip pk_copy_loop): ROM/WRAM/VRAM sources, VRAM/WRAM/overlapping/HRAM/OAM destinations,
+    VBlank/STAT/timer interrupts inside copies, LCD-off copies (fuzz.py copydata_rom); whole v9
+    state vs the oracle at the small launch shape and the benchmarked 512-thread shapes."""
+    from pokegym_amd.testrom.fuzz import copydata_rom
+    lanes, block = shape
+    if lanes:
+        monkeypatch.setenv("PK_WAVE_LANES", lanes)
+        monkeypatch.setenv("PK_K1_BLOCK", block)
+    n = 256
+    gpu, ref = _run_both(copydata_rom(), None, n, 6, 17)
+    bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
+    assert not bad, bad[:4]

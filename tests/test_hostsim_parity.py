@@ -71,3 +71,11 @@ def test_hostsim_map_load_warp():
     assert not bad, bad
     # the recorded envs did warp: wMapSeed (0xD4A1, v9 WRAM at 101285) moved on from its boot value
     assert ref[0][101285 + 0x14A1] != 0x5A
+
+
+def test_hostsim_copydata_block_path():
+    """CopyData (pokered home/copy.asm) and its B/C twin, which K1 runs in blocks of whole passes:
+    ROM/WRAM/VRAM sources, VRAM/WRAM/overlapping/HRAM/OAM destinations, interrupts and the timer
+    landing inside copies, LCD-off copies (pokegym_amd/testrom/fuzz.py copydata_rom)."""
+    from pokegym_amd.testrom.fuzz import copydata_rom
+    assert check(copydata_rom(), 16, 4, 7) == []
