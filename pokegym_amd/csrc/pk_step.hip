@@ -401,11 +401,19 @@ __device__ __forceinline__ void pk_write_slow(const PkStepArgs* A, u8* g, u32 la
 // pending, timer off, their cycles (and the next instruction's) below the next LCD event (LCD off:
 // the frame end) and inside the watchdog budget; code in staged ROM; source in staged ROM, VRAM
 // or WRAM, destination in VRAM or WRAM (no echo, OAM, HRAM or IO), disjoint; no rendered lines
-// pending.  Returns the passes' cycles (0: not taken).
+// pending.  Returns the passes run.
 #define PK_COPY_W0 0x0B13122Au          // 2A 12 13 0B: ld a,[hli] / ld [de],a / inc de / dec bc
 #define PK_COPY_W1A 0xF820B079u         // 79 B0 20 F8: ld a,c / or b / jr nz,-8 (pokered)
 #define PK_COPY_W1B 0xF820B178u         // 78 B1 20 F8: ld a,b / or c / jr nz,-8
 #define PK_COPY_CAP 64u
+// advance a running CPU by `cyc` cycles of `ninstr` instructions inside one LCD event window:
+// DIV, clock, watchdog budget (cycles + 1 per instruction) and the instruction count
+__device__ __forceinline__ void pk_skip(St& s, int& slack, u32& icount, u32 cyc, u32 ninstr) {
+    s.divacc = (s.divacc + cyc) & 0xFFFFu;
+    s.clock += cyc;
+    slack -= (int)(cyc + ninstr);
+    icount += ninstr;
+}
 __device__ __forceinline__ bool copy_ram(u32 a) { return (a - 0x8000u < 0x2000u) | (a - 0xC000u < 0x2000u); }
 __device__ __forceinline__ u32 pk_copy_loop(St& s, const Ctx& c, u32 pc, int& slack, u32& icount) {
     const u32 cpu = s.cpu;
@@ -456,9 +464,43 @@ __device__ __forceinline__ u32 pk_copy_loop(St& s, const Ctx& c, u32 pc, int& sl
     const u32 a = (nbc >> 8) | (nbc & 0xFFu);
     s.w0 = nbc | (((de + k) & 0xFFFFu) << 16);
     s.w1 = ((hl + k) & 0xFFFFu) | (sel(a == 0u, 0x80u, 0u) << 16) | (a << 24);
-    slack -= (int)(7u * k);                            // the tail subtracts the cycles
-    icount += 7u * k;
-    return 52u * k;
+    pk_skip(s, slack, icount, 52u * k, 7u * k);
+    return k;
+}
+
+// The LY poll: pokered's DisableLCD waits for the VBlank line with
+//     ldh a,[rLY] / cp N / jr nz,-6
+// (pkbench's door warp too).  LY changes only at an LCD event or, in a folded frame (see
+// lcd_unfold), every 456 cycles of the clock; while it stays unequal to N every pass reads the
+// same value and sets the same A and flags, so the passes up to the next change (or PK_POLL_CAP)
+// run here in one step; the iteration then executes the next pass's ldh at the advanced clock.
+// Same conditions as the block copy (CPU running, nothing pending, timer off, inside the watchdog
+// budget); staged-ROM code.  Returns the passes skipped.
+#define PK_POLL_W0 0x00FE44F0u          // F0 44 FE: ldh a,[rLY] / cp N (N in the fourth byte)
+#define PK_POLL_W1 0xFA20u              // 20 FA: jr nz,-6
+#define PK_POLL_CAP 256u
+__device__ __forceinline__ u32 pk_poll_loop(St& s, const Ctx& c, u32 pc, u32 bytes, int& slack, u32& icount) {
+    const u32 cpu = s.cpu;
+    if ((cpu & (CPU_CRASH | CPU_HALT | CPU_QUEUED)) | ((cpu >> 8) & (cpu >> 16) & 0x1Fu)) return 0;
+    if (s.tim0 & (4u << 24)) return 0;
+    if (!rom_staged(s, pc) || (pc & 0x3FFFu) > 0x3FFAu) return 0;
+    const u32 li = rom_lds_index(s, pc) + 4u;
+    if ((lds_rom[li] | ((u32)lds_rom[li + 1u] << 8)) != PK_POLL_W1) return 0;
+    const u32 n = bytes >> 24, v = io_read(c, s, 0xFF44u);
+    if (v == n) return 0;
+    // the clock of the first read; LY holds until `chg`, no event before `lim`
+    const u32 c0 = s.clock, lim = sel(s.lcd0 & 0x80u, s.target, FRAME_CYCLES);
+    u32 chg = lim;
+    if (s.lcd2 & PK_LCD_FFOLD) chg = min(chg, s.target - 456u * ((s.target - c0 - 1u) / 456u));
+    if (chg <= c0 || slack < 16) return 0;
+    u32 k = min(PK_POLL_CAP, (chg - c0 - 1u) / 32u + 1u);   // reads at c0 + 32p < chg
+    k = min(k, (lim - c0 - 1u) / 32u);                        // passes end before the event
+    k = min(k, (u32)(slack - 16) / 35u);                      // 32 cycles + 3 instructions each
+    if (k == 0u) return 0;
+    const u32 f = 0x40u | sel((v & 0xFu) < (n & 0xFu), 0x20u, 0u) | sel(v < n, 0x10u, 0u);
+    s.w1 = (s.w1 & 0xFFFFu) | (f << 16) | (v << 24);
+    pk_skip(s, slack, icount, 32u * k, 3u * k);
+    return k;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -839,11 +881,13 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         ev |= sel(exec, PK_EV_EXEC | sel((bytes & 0xFFu) == 0xCBu, PK_EV_CB, 0u), 0u) | sel(pf != 0u, PK_EV_F_LDS, 0u)
             | sel(dispatch, PK_EV_INT, 0u) | sel(!exec && !dispatch, PK_EV_IDLE, 0u);
         if (exec) PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, bytes & 0xFFu);
-        // ---------------- block copy: the CopyData loop (pk_copy_loop) ----------------
+        // ---------------- block copy and LY poll (pk_copy_loop, pk_poll_loop) ----------------
         // whole passes of the loop run here; the iteration then executes the next pass's first
         // instruction as usual (the loop's first bytes identify it: no INT pseudo-op has them)
-        u32 bcyc = 0;
-        if (PK_RARE(bytes == PK_COPY_W0)) bcyc = pk_copy_loop(s, c, pc, slack, icount);
+        if (PK_RARE((bytes == PK_COPY_W0) | ((bytes & 0x00FFFFFFu) == PK_POLL_W0))) {
+            if (bytes == PK_COPY_W0) pk_copy_loop(s, c, pc, slack, icount);
+            else pk_poll_loop(s, c, pc, bytes, slack, icount);
+        }
         const Mc m = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y, e2.z, e2.w, e3.x, e3.y, e3.z, e3.w};
         const u32 D = m.D;
         // the successor's secondary-op entry (read now: its LDS latency overlaps the execute stage)
@@ -853,7 +897,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         // ---------------- execute ----------------
         Ex x;
         pk_exec<PRIO>(s, c, pc, bytes, m, ev, x PK_STAMP_ARGS);
-        u32 cycles = x.cycles + bcyc;
+        u32 cycles = x.cycles;
         const bool wr = x.wr, wram = x.wram;
         // ---------------- fused secondary op (pk_ucode.h pk_u2_entry) ----------------
         // The instruction after this one, if it is a JR (cc), LD r,r', INC/DEC r, INC/DEC BC/DE/HL or
