@@ -113,7 +113,7 @@ def _cpu_baseline(rom: bytes, state, seconds_target: float = 10.0):
     v72, wall72, ips72 = _cpu_run(rom, state, 72, 1, steps72, 2000)
     steps_s = max(4, int(seconds_target / 4 / per_step))
     vs, walls, _ = _cpu_run(rom, state, share, 4, steps_s, 1000)
-    inten = oracle.intensity(rom, state, 32, 3, 8, 99)   # 256 env-steps of the same action stream
+    inten = oracle.intensity(rom, state, 128, 3, 16, 99)   # 2,048 env-steps of the same action stream
     return {
         "value": round(v72, 1),
         "unit": "env-steps/s",
@@ -130,7 +130,10 @@ def _cpu_baseline(rom: bytes, state, seconds_target: float = 10.0):
                       "host_cpus": os.cpu_count()},
         "share_sized_run": {"value": round(vs, 1), "procs": share, "envs_per_proc": 4, "steps": steps_s,
                             "pool_wall_s": round(walls, 1)},
-        "workload_intensity": {k: round(v, 4) for k, v in inten.items()},
+        "workload_intensity": {**{k: round(v, 6) for k, v in inten.items()},
+                               "sample": "C oracle, 128 envs x 16 env-steps (after 3) of the CPU baseline's action stream; "
+                                         "door warps (LCD off for several frames) run in ~0.1% of env-steps "
+                                         "(tools/warp_rate.py: 11 LCD-off frames per 1,000 env-steps over 81,920)"},
     }
 
 

@@ -968,6 +968,18 @@ int gb_batch_run(const uint8_t* rom, uint32_t rom_len, const uint8_t* state, uin
     return 0;
 }
 
+/* The benchmark action stream: action (0-7) of env e at env-step t, the top 3 bits of a splitmix64
+   finalizer over (seed, e, t).  (A plain xor of the three products, used before, gave each env a
+   structured action sequence that never walked through a door in 16,896 env-steps; numpy random
+   actions warp in ~0.1 % of them, as the GPU bench's Philox actions do.) */
+static inline int bench_action(uint32_t seed, uint32_t e, uint32_t t) {
+    uint64_t z = (((uint64_t)seed << 42) ^ ((uint64_t)e << 21) ^ (uint64_t)t) + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (int)(z >> 61);
+}
+
 /* CPU baseline ("port"): n envs, `warmup` untimed env-steps, then `steps` timed env-steps with
  * uniform random actions 0..7 from a counter-based hash of (seed, env, t).  Single thread.
  * Returns elapsed seconds of the timed part; *instr_out = emulated instructions in it. */
@@ -978,7 +990,7 @@ double gb_bench(const uint8_t* rom, uint32_t rom_len, const uint8_t* state, uint
     if (state && gb_load_state(tmpl, state, state_len)) { gb_free(tmpl); return -2.0; }
     gb_t** envs = (gb_t**)calloc(n, sizeof(gb_t*));
     for (uint32_t e = 0; e < n; e++) envs[e] = gb_clone(tmpl);
-    #define ACT(e, t) ((int)((((uint64_t)(seed) * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)(e) * 0xBF58476D1CE4E5B9ull) ^ ((uint64_t)(t) * 0x94D049BB133111EBull)) >> 61))
+    #define ACT(e, t) bench_action(seed, (e), (t))
     for (uint32_t t = 0; t < warmup; t++)
         for (uint32_t e = 0; e < n; e++) gb_run_action(envs[e], ACT(e, t), 24, 8);
     uint64_t i0 = 0;
@@ -1000,13 +1012,14 @@ double gb_bench(const uint8_t* rom, uint32_t rom_len, const uint8_t* state, uint
 /* Workload intensity of the bench's action stream (the same actions as gb_bench): out[0] emulated
  * instructions, [1] ticks, [2] cycles, [3] cycles spent halted (HALT fast-forward), [4] cycles with
  * the LCD off, [5] frames — summed over n envs x steps env-steps after warmup. */
+
 int gb_intensity(const uint8_t* rom, uint32_t rom_len, const uint8_t* state, uint32_t state_len,
                  uint32_t n, uint32_t warmup, uint32_t steps, uint32_t seed, uint64_t* out) {
     gb_t* tmpl = gb_new(rom, rom_len);
     if (!tmpl) return -1;
     if (state && gb_load_state(tmpl, state, state_len)) { gb_free(tmpl); return -2; }
     for (int k = 0; k < 6; k++) out[k] = 0;
-    #define ACT(e, t) ((int)((((uint64_t)(seed) * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)(e) * 0xBF58476D1CE4E5B9ull) ^ ((uint64_t)(t) * 0x94D049BB133111EBull)) >> 61))
+    #define ACT(e, t) bench_action(seed, (e), (t))
     for (uint32_t e = 0; e < n; e++) {
         gb_t* g = gb_clone(tmpl);
         for (uint32_t t = 0; t < warmup; t++) gb_run_action(g, ACT(e, t), 24, 8);
