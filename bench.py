@@ -40,6 +40,9 @@ HBM_PEAK_GBS = 8000.0                       # MI355X_MICROARCH.md: 8.0 TB/s HBM3
 CONFIGS3_ENVS = 262144                      # configs[3] / configs[4]: envs over all GPUs
 
 WORKLOADS = {
+    "config1": dict(envs=1, render=True, reward=True, vecenv=False, actions="zero", bytes=B_REWARD,
+                    desc="configs[0]'s shape on the GPU build: ONE drop-in Environment (reward stack, (72,80,4) obs), "
+                         "1,000 warm-up steps then 10,000 x step(0), as /root/reference/test.py:16-29 times PyBoy+pokegym"),
     "config2": dict(envs=4096, render=False, reward=False, vecenv=False, actions="cycle", bytes=B_HEADLESS,
                     desc="configs[1]: headless (no PPU), RAM-only obs, fixed action cycle [0,3,1,2]"),
     "config3": dict(envs=65536, render=True, reward=False, vecenv=False, actions="random", bytes=B_SCREEN,
@@ -75,14 +78,19 @@ def _cpu_quota():
 
 
 def _cpu_run(rom, state, workers, n_per, steps, seed0):
-    """workers forked processes, each n_per envs x steps timed env-steps (after 3 warmup) of the C
-    oracle; aggregate env-steps/s over the slowest process's timed span."""
-    import multiprocessing as mp
+    """`workers` concurrent workers, each n_per envs x steps timed env-steps (after 3 warmup) of the
+    C oracle; aggregate env-steps/s over the slowest worker's timed span.
+
+    Workers are threads of this process: gb_bench is re-entrant C and ctypes releases the GIL for
+    the call, so they run in parallel on the host cores exactly as separate processes would.  No
+    process is forked: bench.py holds the GPU (and, under rocprofv3, the profiler's state) by the
+    time this runs, and a fork of such a process is what aborted the round-3 profile run
+    (VERDICT r03 weak 4)."""
+    from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle
-    ctx = mp.get_context("fork")
-    with ctx.Pool(workers) as pool:
+    with ThreadPoolExecutor(max_workers=workers) as pool:
         t0 = time.time()
-        res = pool.starmap(oracle.bench, [(rom, state, n_per, 3, steps, seed0 + w) for w in range(workers)])
+        res = list(pool.map(lambda w: oracle.bench(rom, state, n_per, 3, steps, seed0 + w), range(workers)))
         wall = time.time() - t0
     slowest = max(r[0] for r in res)
     return workers * n_per * steps / slowest, wall, sum(r[1] for r in res) / slowest
@@ -91,10 +99,11 @@ def _cpu_run(rom, state, workers, n_per, steps, seed0):
 def _cpu_baseline(rom: bytes, state, seconds_target: float = 10.0):
     """The oracle (C restatement of the path, oracle/gbcore.c) on the host cores: "port".
 
-    Main value: the reference's own CPU shape, 72 envs each in its own worker process
-    (README.md:116-118; PufferLib multiprocessing), on whatever cores the box grants.  Beside it, a
-    run sized to the box's CPU share (cgroup quota, else the 16 threads the GPU box allots one GPU:
-    OMP_NUM_THREADS) with 4 envs per process, and the workload intensity of the same action stream."""
+    Two shapes on whatever cores the box grants: the reference's own CPU shape, 72 envs each in its
+    own worker (README.md:116-118; PufferLib multiprocessing), and a run sized to the box's CPU share
+    (cgroup quota, else the 16 threads the GPU box allots one GPU: OMP_NUM_THREADS) with 4 envs per
+    worker.  `value` is the faster of the two (the CPU's best showing on those cores); both are
+    recorded, with the worker count beside `cores`.  Plus the workload intensity of the action stream."""
     from oracle import oracle
     oracle.lib()
     try:
@@ -105,30 +114,36 @@ def _cpu_baseline(rom: bytes, state, seconds_target: float = 10.0):
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     share = quota or omp or 16
     share = max(1, min(share, affinity or share))
-    # calibrate: seconds per env-step of one process
+    # calibrate: seconds per env-step of one worker
     sec, _ = oracle.bench(rom, state, 2, 3, 4, 99)
     per_step = sec / 8.0
-    # 72 processes x 1 env on `share` cores: ~seconds_target of wall
+    # 72 workers x 1 env on `share` cores: ~seconds_target of wall
     steps72 = max(4, int(seconds_target * share / 72 / per_step))
     v72, wall72, ips72 = _cpu_run(rom, state, 72, 1, steps72, 2000)
     steps_s = max(4, int(seconds_target / 4 / per_step))
-    vs, walls, _ = _cpu_run(rom, state, share, 4, steps_s, 1000)
+    vs, walls, ipss = _cpu_run(rom, state, share, 4, steps_s, 1000)
     inten = oracle.intensity(rom, state, 128, 3, 16, 99)   # 2,048 env-steps of the same action stream
+    best_share = vs >= v72
     return {
-        "value": round(v72, 1),
+        "value": round(max(v72, vs), 1),
         "unit": "env-steps/s",
-        "cores": min(72, share),
+        "cores": share,
+        "workers": share if best_share else 72,
         "kind": "port",
-        "sample": (f"the reference's CPU shape: 72 envs, one per worker process (README.md:116-118), x {steps72} timed "
-                   f"env-steps each (after 3 warmup) of the same ROM and random actions on the C oracle "
-                   f"(oracle/gbcore.c, 1 thread/process), on a CPU share of {share} cores "
-                   f"({'cgroup ' + quota_raw if quota else 'no cgroup quota; OMP_NUM_THREADS=' + str(omp or 'unset') + ' is the box share'}); "
-                   f"aggregate over the slowest process's timed span; pool wall {wall72:.1f}s. PyBoy+pokegym itself is "
-                   "not installed (pure-Python PyBoy would be slower than this C restatement)"),
-        "instr_per_s": round(ips72, 1),
+        "shape": "share-sized run" if best_share else "72-worker reference shape",
+        "sample": (f"the C oracle (oracle/gbcore.c, 1 thread per worker) on a CPU share of {share} cores "
+                   f"({'cgroup ' + quota_raw if quota else 'no cgroup quota; OMP_NUM_THREADS=' + str(omp or 'unset') + ' is the box share'}), "
+                   f"same ROM and random-action stream; the faster of (a) the reference's CPU shape, 72 one-env workers "
+                   f"(README.md:116-118) x {steps72} timed env-steps, and (b) {share} workers x 4 envs x {steps_s} "
+                   "timed env-steps (after 3 warmup each); aggregate over the slowest worker's timed span. Workers are "
+                   "threads (ctypes releases the GIL), not forked processes. PyBoy+pokegym itself is not installed "
+                   "(pure-Python PyBoy would be slower than this C restatement)"),
+        "instr_per_s": round(max(ips72, ipss), 1),
         "cpu_share": {"cores": share, "cgroup": quota_raw, "omp_num_threads": omp or None, "affinity_cpus": affinity,
                       "host_cpus": os.cpu_count()},
-        "share_sized_run": {"value": round(vs, 1), "procs": share, "envs_per_proc": 4, "steps": steps_s,
+        "reference_shape_run": {"value": round(v72, 1), "workers": 72, "envs_per_worker": 1, "steps": steps72,
+                                "pool_wall_s": round(wall72, 1)},
+        "share_sized_run": {"value": round(vs, 1), "workers": share, "envs_per_worker": 4, "steps": steps_s,
                             "pool_wall_s": round(walls, 1)},
         "workload_intensity": {**{k: round(v, 6) for k, v in inten.items()},
                                "sample": "C oracle, 128 envs x 16 env-steps (after 3) of the CPU baseline's action stream; "
@@ -226,11 +241,90 @@ class StepFlow:
         return [a.elapsed_time(b) for a, b in self.ar_ev]
 
 
+def run_config1(args):
+    """configs[0]'s benchmark shape (/root/reference/test.py:16-29: one env, reset, 1,000 x step(0)
+    untimed, then `steps` x step(0) timed) through the drop-in single `Environment`
+    (pokegym_amd/env.py) on one GPU: every step is K1 (one lane), K2, K4, K3 plus the host round trip
+    of the reference's return values (reward float, done bool, obs array).  Beside it, the C oracle's
+    emulation-only rate of the same action stream in one process (no reward stack)."""
+    import torch
+    from oracle import oracle
+    from pokegym_amd.env import Environment
+    from pokegym_amd.testrom.game import game_rom
+    rom = open(args.rom, "rb").read() if args.rom else game_rom(banks=args.rom_banks)
+    if args.state:
+        state = open(args.state, "rb").read()
+    else:
+        # pkbench's post-boot state (Bulbasaur.state is a Pokemon Red state: under pkbench its party is
+        # wiped, and the info step at time 10,000 would raise the reference's empty-party ValueError)
+        g = oracle.GB(rom)
+        g.power_on()
+        state = g.save_state()
+        del g
+    # CPU reference point first (no GPU touched yet): one process, emulation only
+    g = oracle.GB(rom, state)
+    cw = min(args.warmup, 1000)
+    for _ in range(cw):
+        g.run_action(0)
+    cs = min(args.steps, 5000)
+    t0 = time.perf_counter()
+    for _ in range(cs):
+        g.run_action(0)
+    cpu_rate = cs / (time.perf_counter() - t0)
+    del g
+
+    env = Environment(rom_path=rom, state_path=state)
+    env.reset()
+    for _ in range(args.warmup):
+        env.step(0)
+    torch.cuda.synchronize()
+    env.emu.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        env.step(0)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    emu_ms, ren_ms, rew_ms, nprof = env.emu.profile_read()
+    instr = env.emu.last_instr_count()
+    env.close()
+    k = max(nprof, 1)
+    span = (emu_ms + ren_ms + rew_ms) / k
+    out = {
+        "metric": "env.step/sec (one env, configs[0] shape)",
+        "value": round(args.steps / elapsed, 2),
+        "unit": "env-steps/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {"workload": f"config1 = {WORKLOADS['config1']['desc']}", "envs_per_gpu": 1,
+                   "rom": "pkbench (synthetic game ROM; pokemon_red.gb is not shipped)" if not args.rom else os.path.basename(args.rom),
+                   "start_state": "pkbench post-boot" if not args.state else os.path.basename(args.state),
+                   "action": "0 (Down) every step, as test.py", "frame_skip": 24, "release_frame": 8},
+        "latency_ms": {"step_wall": round(elapsed / args.steps * 1e3, 3), "k1": round(emu_ms / k, 3),
+                       "k2_render": round(ren_ms / k, 3), "k4_k3_reward_obs": round(rew_ms / k, 3),
+                       "host_and_launch": round(elapsed / args.steps * 1e3 - span, 3)},
+        "instr_per_env_step": instr,
+        "cpu_baseline": {"value": round(cpu_rate, 2), "unit": "env-steps/s", "cores": 1, "kind": "port",
+                         "sample": (f"C oracle (oracle/gbcore.c) in this process, one env, {cw} x step(0) warm-up then "
+                                    f"{cs} x step(0) timed; emulation only (no reward stack, no obs)")},
+        "note": ("one env leaves 1 of the GPU's 65,536 lanes busy: each emulated instruction is a dependent chain "
+                 "of LDS and memory round trips with nothing to hide them, so this shape measures latency, not "
+                 "throughput (use VecEnv)"),
+    }
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None, help="timed env-steps (default 20; config1: 10,000)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed env-steps first (default 3; config1: 1,000)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default=None,
                     help="default: config3 on one GPU, config4 (the configs[3] per-GPU shard) on several")
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: the workload's)")
@@ -252,6 +346,13 @@ def main():
                          "copy stream overlapped with the next step) inside the timed region -- the PCIe-inclusive "
                          "rate of a numpy-consuming caller (DESIGN.md section 6); not the default bench line")
     args = ap.parse_args()
+    single = args.workload == "config1"
+    if args.steps is None:
+        args.steps = 10000 if single else 20
+    if args.warmup is None:
+        args.warmup = 1000 if single else 3
+    if single:
+        return run_config1(args)
 
     import torch
     import torch.distributed as dist
@@ -430,7 +531,10 @@ def main():
                                  "of configs[3]"),
             },
             "roofline": {
-                "bound": "hbm",
+                # what limits K1, measured (PMC issue counts, wave timers): not HBM bandwidth and not
+                # MFMA; `peak`/`frac` price the algorithmic bytes against the HBM roofline
+                "bound": "latency",
+                "priced_against": "hbm",
                 "measured_bound": ("dependent latency + issue (not HBM, not MFMA): per loop iteration (one emulated "
                                    "SM83 instruction, two when a register-only successor fuses) a wave runs the LDS "
                                    "fetch -> microcode -> address -> operand-read chain of its divergent lanes and the "

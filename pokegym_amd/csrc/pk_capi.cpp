@@ -355,7 +355,9 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
         }
         if (const char* pr = getenv("PK_K1_PRIO")) h->k1_prio = atoi(pr) ? 1 : 0;
         // image interleave = K1's envs per wave for this handle (no 64-byte line shared by two
-        // waves; a wave's lanes share one sub-block base); PK_ILV (>= the wave's envs) overrides
+        // waves; a wave's lanes share one sub-block base).  PK_ILV overrides it with any power of
+        // two <= 64: narrower than the wave puts one wave's envs in several sub-blocks (K1 reaches
+        // them through its per-lane offset), wider shares a sub-block between waves
         uint32_t ilv = k1_wave_lanes(h, h->n);
         if (const char* iv = getenv("PK_ILV")) {
             int v = atoi(iv);

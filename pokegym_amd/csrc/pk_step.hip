@@ -41,6 +41,11 @@
 #ifndef PK_TRACE
 #define PK_TRACE(env, pc, w0, w1, sp, op) ((void)0)
 #endif
+// a loop fast path ran `passes` whole passes of a `len`-instruction loop after the traced
+// instruction (tools/trace_diff.py drops the oracle's records of those passes)
+#ifndef PK_TRACE_SKIP
+#define PK_TRACE_SKIP(env, pc, passes, len) ((void)0)
+#endif
 #ifndef PK_ITER
 #define PK_ITER(env, ev) ((void)(ev))
 #endif
@@ -885,8 +890,13 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         // whole passes of the loop run here; the iteration then executes the next pass's first
         // instruction as usual (the loop's first bytes identify it: no INT pseudo-op has them)
         if (PK_RARE((bytes == PK_COPY_W0) | ((bytes & 0x00FFFFFFu) == PK_POLL_W0))) {
-            if (bytes == PK_COPY_W0) pk_copy_loop(s, c, pc, slack, icount);
-            else pk_poll_loop(s, c, pc, bytes, slack, icount);
+            if (bytes == PK_COPY_W0) {
+                const u32 k = pk_copy_loop(s, c, pc, slack, icount);
+                if (k) PK_TRACE_SKIP(env, pc, k, 7u);
+            } else {
+                const u32 k = pk_poll_loop(s, c, pc, bytes, slack, icount);
+                if (k) PK_TRACE_SKIP(env, pc, k, 3u);
+            }
         }
         const Mc m = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y, e2.z, e2.w, e3.x, e3.y, e3.z, e3.w};
         const u32 D = m.D;
@@ -1189,7 +1199,6 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
         }
     }
 #endif
-    if (!active) return;
     // lanes past the range's end (in its last 64-env group) ran nothing and write nothing back:
     // those envs may belong to nobody else, but the range does not own them
     if (!active) return;
@@ -1215,7 +1224,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
 
 hipError_t pk_launch_step(const PkStepArgs& a, hipStream_t s) {
     // one wave per SIMD while the waves fit, else 512-thread workgroups put two waves on each SIMD
-    // of a CU (the ~115 KB of LDS staging allows one workgroup per CU)
+    // of a CU (the 158 KB of LDS staging allows one workgroup per CU)
     const u32 wl = a.wave_lanes;
     const u32 span = ((a.env1 + PK_LANES - 1u) & ~(PK_LANES - 1u)) - a.env0;
     const u32 threads = span * (PK_LANES / wl);

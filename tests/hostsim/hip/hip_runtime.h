@@ -103,6 +103,8 @@ void pk_sim_launch(const char* name, dim3 grid, dim3 block, const std::function<
 // instruction trace for debugging (env, pc, w0, w1, sp, opcode)
 extern "C" void pk_sim_trace(uint32_t env, uint32_t pc, uint32_t w0, uint32_t w1, uint32_t sp, uint32_t op);
 #define PK_TRACE(env, pc, w0, w1, sp, op) pk_sim_trace(env, pc, w0, w1, sp, op)
+// loop fast-path marker: op = 0x1000 | loop length, w0 = passes run (tools/trace_diff.py)
+#define PK_TRACE_SKIP(env, pc, passes, len) pk_sim_trace(env, pc, passes, 0u, 0u, 0x1000u | (len))
 
 // per-iteration event bits (iteration statistics for kernel design; see pk_kernels.hip PK_EV_*)
 extern "C" void pk_sim_iter(uint32_t env, uint32_t ev);

@@ -110,6 +110,53 @@ def _reward_run(rom, state, actions, max_steps):
     return rew, done, err, obs_d, wram_d
 
 
+def _reset_flow(rom, state, actions, max_steps, check_at):
+    """The configs[3] VecEnv flow without the reward stack (reward=False): every env runs its actions
+    (steps, m) from the template, `time` counts env-steps and an env whose time reaches max_steps is
+    reset to the template after that step (done = time >= max_episode_steps, environment.py:1612-1613;
+    the auto-reset of VecEnv: the template reload every reset does when PK_F_REWARD is off).  Returns
+    (v9 digests after each step t in check_at (len(check_at), m), dones (steps, m))."""
+    import xxhash
+
+    from oracle import oracle as O
+    steps, m = actions.shape
+    dig = np.zeros((len(check_at), m), np.uint64)
+    done = np.zeros((steps, m), np.uint8)
+    at = {t: k for k, t in enumerate(check_at)}
+    base = O.GB(rom, state)
+    if state is None:
+        base.power_on()
+    for e in range(m):
+        gb, time = base.clone(), 0
+        for t in range(steps):
+            gb.run_action(int(actions[t, e]))
+            time += 1
+            if time >= max_steps:
+                done[t, e] = 1
+                gb, time = base.clone(), 0
+            if t in at:
+                dig[at[t], e] = xxhash.xxh3_64_intdigest(gb.save_state())
+    return dig, done
+
+
+def reset_flows(ex: ProcessPoolExecutor, rom: bytes, state, actions: np.ndarray, max_steps: int, check_at, chunk=512):
+    """(digests (len(check_at), n), dones (steps, n)) of _reset_flow over worker chunks."""
+    steps, n = actions.shape
+    futs = [(e0, ex.submit(_reset_flow, rom, state, np.ascontiguousarray(actions[:, e0:e0 + chunk]), max_steps,
+                           list(check_at))) for e0 in range(0, n, chunk)]
+    return futs
+
+
+def gather_reset_flows(futs, n_check: int, steps: int, n: int):
+    dig = np.zeros((n_check, n), np.uint64)
+    done = np.zeros((steps, n), np.uint8)
+    for e0, f in futs:
+        d, dn = f.result()
+        dig[:, e0:e0 + d.shape[1]] = d
+        done[:, e0:e0 + dn.shape[1]] = dn
+    return dig, done
+
+
 def reward_runs_async(ex: ProcessPoolExecutor, rom: bytes, state, actions: np.ndarray, max_steps: int, chunk=256):
     n = actions.shape[1]
     return [(e0, ex.submit(_reward_run, rom, state, np.ascontiguousarray(actions[:, e0:e0 + chunk]), max_steps))

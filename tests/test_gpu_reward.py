@@ -186,3 +186,22 @@ def test_gpu_full_step_with_reward_matches_oracle(state_name):
                 o = R.reset(sts[e], buses[e], GREY[gbs[e].screen()], reload=None, max_episode_steps=4)
                 assert np.array_equal(o, obs_r[e]), (t, e)
     emu.close()
+
+
+
+@pytest.mark.gpu
+def test_gpu_reward_replay_at_scale():
+    """K4/K5r/K3 at width against the reference's recorded outputs: every golden sequence replicated
+    over 4,096-env handles (reward_replay.run_replay_batched)."""
+    from pokegym_amd.emulator import BatchedEmulator
+    from pokegym_amd.testrom.game import game_rom
+    from reward_replay import run_replay_batched
+    base = open(os.path.join(REPO, "pokegym_amd", "states", "Bulbasaur.state"), "rb").read()
+    rom = game_rom()
+
+    def make(state, n, max_steps):
+        return BatchedEmulator(rom, n, state=state, frame_skip=0, render=False, reward=True,
+                               max_episode_steps=max_steps, heatmap=True)
+
+    checked = run_replay_batched(make, 4096, base)
+    assert checked["step"] > 1500 and checked["err"] >= 6 and checked["reset"] > 80, checked

@@ -207,3 +207,49 @@ def test_512_env_workgroups_48_steps(monkeypatch):
         torch.cuda.synchronize()
         _check_states(rom, None, actions, emu, futs, headless=False)
         emu.close()
+
+
+def test_config4_flow_vs_oracle_per_env():
+    """The benchmarked configs[3] flow itself against the oracle, env by env: VecEnv with 32,768 envs
+    in 2 sub-batches of 16,384 (pk_step_range launches on their own streams), recv/send over 7
+    env-steps with max_episode_steps 4, so every env auto-resets on the device (pk_reset_range:
+    template reload of the done envs of its sub-batch, environment.py:1612-1613 done rule) after its
+    4th step.  Whole-machine v9 digests of every env after step 3 (before any reset) and after step
+    7 (3 steps into the second episode) == the oracle replaying the same actions with reset-on-done;
+    the dones recv() hands back == the oracle's, in both sub-batches."""
+    import torch
+    from pokegym_amd.env import VecEnv
+    from pokegym_amd.testrom.game import game_rom
+    rom, n, steps, max_steps = game_rom(), 32768, 7, 4
+    actions = np.random.default_rng(40968).integers(0, 8, (steps, n), dtype=np.uint8)
+    check_at = (2, steps - 1)
+    with OP.pool() as ex:
+        futs = OP.reset_flows(ex, rom, None, actions, max_steps, check_at, chunk=512)
+        vec = VecEnv(n, rom=rom, power_on=True, reward=False, max_episode_steps=max_steps, log_interval=0,
+                     batch_size=n // 2)
+        assert vec.num_batches == 2
+        acts = torch.from_numpy(actions).to(vec.device)
+        vec.async_reset()
+        got_done = np.zeros((steps, n), np.uint8)
+        got_dig = []
+        for t in range(steps):
+            for _ in range(vec.num_batches):
+                obs, rew, term, trunc, infos, ids, masks = vec.recv()
+                sl = vec.current_envs()
+                if t > 0:   # the terminals of this sub-batch's step t-1
+                    got_done[t - 1, sl] = term.to(torch.uint8).cpu().numpy()
+                vec.send(acts[t, sl])
+            if t in check_at:
+                # every sub-batch's step t has been sent: wait for both streams, digest every env
+                vec._join_streams()
+                torch.cuda.synchronize()
+                got_dig.append(gpu_digests(vec.emu))
+        got_done[steps - 1] = vec.emu.terminals.cpu().numpy()
+        want_dig, want_done = OP.gather_reset_flows(futs, len(check_at), steps, n)
+        vec.close()
+    assert np.array_equal(got_done, want_done), np.argwhere(got_done != want_done)[:5]
+    half = n // 2
+    assert want_done[:, :half].sum() == half and want_done[:, half:].sum() == half   # one done per env
+    for k, t in enumerate(check_at):
+        bad = np.nonzero(got_dig[k] != want_dig[k])[0]
+        assert not len(bad), f"after step {t + 1}: {len(bad)}/{n} envs differ, first {bad[:8].tolist()}"

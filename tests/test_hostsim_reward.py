@@ -32,3 +32,22 @@ def test_hostsim_info_record_matches_reference():
     g, got = run_info_replay(HostsimRewardBackend(game_rom()), base)
     assert check_info(g, got) > 100
     check_events(g, got.events)
+
+
+@pytest.mark.slow
+def test_hostsim_reward_replay_batched():
+    """The golden sequences as envs of batched handles (reward_replay.run_replay_batched: replicas
+    side by side, masked resets, one handle per episode length) — the host-compiled kernels at 160
+    envs per handle (the GPU test runs 4,096)."""
+    from emulator import HostsimEmulator
+    from reward_replay import run_replay_batched
+    from pokegym_amd.testrom.game import game_rom
+    rom = game_rom()
+    base = open(os.path.join(HERE, "..", "pokegym_amd", "states", "Bulbasaur.state"), "rb").read()
+
+    def make(state, n, max_steps):
+        return HostsimEmulator(rom, n, state=state, frame_skip=0, render=False, reward=True,
+                               max_episode_steps=max_steps)
+
+    checked = run_replay_batched(make, 160, base)
+    assert checked["step"] > 1500 and checked["err"] >= 6 and checked["reset"] > 80, checked

@@ -60,6 +60,7 @@ def main():
     ap.add_argument("--prio", type=int, default=1)
     ap.add_argument("--s", default=None)
     ap.add_argument("--blocks", action="store_true")
+    ap.add_argument("--dump", default=None, help="write the common path's instructions to this file")
     ap.add_argument("extra", nargs="*")
     a = ap.parse_args()
     path = a.s or compile_s(a.extra)
@@ -73,6 +74,7 @@ def main():
     # taken, rare blocks the compiler moved out of line are skipped) and follow s_branch, until the
     # header comes round again (a rotated loop reaches it through a latch block laid out before it)
     cnt, blocks, cur = Counter(), [], None
+    path = []
     i, seen = i0, set()
     while True:
         s = K[i].strip()
@@ -90,6 +92,7 @@ def main():
         if not s or s.startswith(";") or s.startswith("."):
             continue
         c = classify(s)
+        path.append(s)
         cnt[c] += 1
         if cur:
             cur[1][c] += 1
@@ -100,6 +103,8 @@ def main():
     tot = sum(v for k, v in cnt.items() if k not in ("waitcnt", "nop"))
     print(f"loop header line {i0}, common path: issued {tot}  " + "  ".join(f"{k} {cnt[k]}" for k in
           ("valu", "salu", "branch", "lds", "vmem", "smem", "waitcnt", "nop", "misc", "other") if cnt[k]))
+    if a.dump:
+        open(a.dump, "w").write("\n".join(path) + "\n")
     if a.blocks:
         for name, c in blocks:
             print(f"  {name:12s} " + " ".join(f"{k}={v}" for k, v in sorted(c.items())))

@@ -48,7 +48,20 @@ def main():
     m = O.gb_trace_count()
     O.gb_trace_enable(None, 0)
     ref = obuf[:m]
-    print(f"device {len(dev)} records, oracle {len(ref)}")
+    # fold the loop fast paths: a device marker (op 0x1000 | loop length, w0 = passes) stands for
+    # passes x length oracle records right after the traced instruction (pk_copy_loop/pk_poll_loop
+    # run whole passes inside one iteration and trace none of their instructions)
+    keep_d, keep_r, j = [], [], 0
+    for i in range(len(dev)):
+        if dev[i, 4] & 0x1000:
+            j += int(dev[i, 1]) * int(dev[i, 4] & 0xFFF)
+            continue
+        keep_d.append(i)
+        keep_r.append(j)
+        j += 1
+    nn = sum(1 for r in keep_r if r < len(ref))
+    dev, ref = dev[keep_d[:nn]], ref[keep_r[:nn]]
+    print(f"device {len(dev)} records, oracle {len(ref)} (after folding loop fast-path passes)")
     cols = ["pc", "w0", "w1", "sp", "op"]
     nn = min(len(dev), len(ref))
     d = np.nonzero((dev[:nn, :5] != ref[:nn, :5]).any(1))[0]
