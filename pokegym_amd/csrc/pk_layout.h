@@ -30,12 +30,24 @@ typedef struct { uint32_t x, y; } uint2_t;
 
 #define PK_LANES 64u
 #define PK_PHYS 0xC200u
-#define PK_GROUP_STRIDE (PK_PHYS * PK_LANES)
+// sub-block skew: every sub-block starts PK_SKEW bytes after the end of the previous one, so the
+// same guest byte of consecutive sub-blocks (waves) is not at the same offset modulo the memory
+// channel interleave (PK_PHYS << sh is a multiple of 16 KiB for sh >= 5)
+#ifndef PK_SKEW
+#define PK_SKEW 0u
+#endif
+// bytes of one 64-env group: the largest over the interleaves (sh = 0: 64 sub-blocks)
+#define PK_GROUP_STRIDE (PK_PHYS * PK_LANES + PK_SKEW * PK_LANES)
+
+// sub-block stride and group stride of interleave 1 << sh
+__host__ __device__ static inline uint64_t pk_sub_stride(uint32_t sh) { return ((uint64_t)PK_PHYS << sh) + PK_SKEW; }
+__host__ __device__ static inline uint64_t pk_group_stride(uint32_t sh) { return (uint64_t)(PK_LANES >> sh) * pk_sub_stride(sh); }
 
 // byte offset of (env, phys) in the image array, interleave 1 << sh
 __host__ __device__ static inline uint64_t pk_img_off(uint32_t env, uint32_t phys, uint32_t sh) {
     const uint32_t l = env & (PK_LANES - 1u);
-    return (uint64_t)(env / PK_LANES) * PK_GROUP_STRIDE + (((uint64_t)(l >> sh) * PK_PHYS + phys) << sh) + (l & ((1u << sh) - 1u));
+    return (uint64_t)(env / PK_LANES) * pk_group_stride(sh) + (uint64_t)(l >> sh) * pk_sub_stride(sh)
+         + ((uint64_t)phys << sh) + (l & ((1u << sh) - 1u));
 }
 
 #define PK_P_VRAM 0x0000u
@@ -83,8 +95,12 @@ enum {
 #ifndef PK_K1_MAX_THREADS
 #define PK_K1_MAX_THREADS 512
 #endif
+#ifndef PK_WG_ENVS
 #define PK_WG_ENVS 512u
+#endif
+#ifndef PK_LDS_SLOTS
 #define PK_LDS_SLOTS 6u  // ROM banks (16 KiB each) staged in LDS by the step kernel (slot 0 = bank 0)
+#endif
 
 // kernel argument blocks (passed by value)
 struct PkStepArgs {

@@ -746,8 +746,8 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
     // wave puts the wave's envs in several sub-blocks, reached through the per-lane offset
     {
         const u32 sub = c.glane >> c.sh, sub0 = __builtin_amdgcn_readfirstlane(sub);
-        c.g = A.mem + (size_t)c.gid * PK_GROUP_STRIDE + (((size_t)sub0 * PK_PHYS) << c.sh);
-        c.lane = (((sub - sub0) * PK_PHYS) << c.sh) + (c.glane & ((1u << c.sh) - 1u));
+        c.g = A.mem + (size_t)c.gid * pk_group_stride(c.sh) + (size_t)sub0 * pk_sub_stride(c.sh);
+        c.lane = (u32)((sub - sub0) * pk_sub_stride(c.sh)) + (c.glane & ((1u << c.sh) - 1u));
     }
     c.loc = (threadIdx.x >> 6) * A.wave_lanes + wl;  // < PK_WG_ENVS envs per workgroup
     for (u32 i = 0; i < PK_HC_ROWS; i++) lds_rom[PK_HC_BASE + c.loc * PK_HC_STRIDE + i] = (u8)ld_img(c, PK_P_HRAM + i);

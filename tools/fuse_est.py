@@ -42,6 +42,14 @@ def secondary(op):
     return op in (0xC6, 0xCE, 0xD6, 0xDE, 0xE6, 0xEE, 0xF6, 0xFE)
 
 
+MEMW = {0x02, 0x12, 0x22, 0x32, 0x70, 0x71, 0x72, 0x73, 0x74, 0x75, 0x77}   # ld (rr),a / ld (hl),r
+
+
+def writes_mem(op):
+    return op in MEMW or op in (0x34, 0x35, 0x36, 0xE0, 0xE2, 0xEA, 0x08) or op in (0xC5, 0xD5, 0xE5, 0xF5, 0xCD, 0xC4,
+                                                                             0xCC, 0xD4, 0xDC)
+
+
 def primary_fusable(op):
     ctrl = {0x18, 0x20, 0x28, 0x30, 0x38, 0xC0, 0xC2, 0xC3, 0xC4, 0xC7, 0xC8, 0xC9, 0xCA, 0xCC, 0xCD, 0xCF, 0xD0,
             0xD2, 0xD4, 0xD7, 0xD8, 0xD9, 0xDA, 0xDC, 0xDF, 0xE7, 0xE9, 0xEF, 0xF7, 0xFF, 0xF3, 0xFB, 0x76, 0x10,
@@ -49,7 +57,7 @@ def primary_fusable(op):
     return op not in ctrl
 
 
-def groups(tr, slots, fetch):
+def groups(tr, slots, fetch, memw=False):
     """tr: list of (pc, op); returns the number of loop iterations"""
     n, i, it = len(tr), 0, 0
     while i < n:
@@ -60,7 +68,8 @@ def groups(tr, slots, fetch):
             k = 0
             while k < slots - 1 and j < n:
                 pc2, op2 = tr[j]
-                if pc2 != (tr[j - 1][0] + ilen(tr[j - 1][1])) & 0xFFFF or not secondary(op2):
+                ok2 = secondary(op2) or (memw and op2 in MEMW and not writes_mem(op))
+                if pc2 != (tr[j - 1][0] + ilen(tr[j - 1][1])) & 0xFFFF or not ok2:
                     break
                 if used + ilen(op2) > fetch or pc >= 0x8000:
                     break
@@ -98,12 +107,15 @@ def main():
     buf = (ctypes.c_uint32 * (6 * cap))()
     m = L.pk_sim_trace_get(buf, cap)
     a = np.frombuffer(buf, dtype=np.uint32, count=6 * m).reshape(m, 6)
-    tr = [(int(r[0]), int(r[4]) & 0xFF) for r in a]
+    tr = [(int(r[0]), int(r[4]) & 0xFF) for r in a if not (int(r[4]) & 0x1000)]   # drop loop fast-path markers
     emu.close()
     print(f"env {env} {'warp ' if warp else ''}{steps} steps: {len(tr)} instructions")
     for slots, fetch in ((1, 4), (2, 4), (3, 4), (2, 8), (3, 8), (4, 8)):
         it = groups(tr, slots, fetch)
         print(f"  slots={slots} fetch={fetch}B: iterations {it}  ({it / max(len(tr), 1):.3f} per instruction)")
+    it = groups(tr, 2, 4, memw=True)
+    print(f"  slots=2 fetch=4B + memory-write secondaries (ld (rr),a / ld (hl),r after a non-writing primary): "
+          f"iterations {it}  ({it / max(len(tr), 1):.3f} per instruction)")
 
 
 if __name__ == "__main__":
