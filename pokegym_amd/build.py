@@ -34,10 +34,13 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None, ex
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
     objs = []
-    for src in SOURCES:
-        obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + (".alt.o" if out else ".o"))
+    # (source, object stem, extra defines): K1 is compiled twice, the default kernel and the
+    # small-LDS kernel for concurrent sub-batch ranges (pk_layout.h PK_K1_SMALL)
+    units = [(src, os.path.splitext(src)[0], []) for src in SOURCES] + [("pk_step.hip", "pk_step_small", ["-DPK_K1_SMALL"])]
+    for src, stem, defs in units:
+        obj = os.path.join(LIBDIR, stem + (".alt.o" if out else ".o"))
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-               "-Wno-unused-function", "-Wno-bitwise-instead-of-logical", "-c", "-o", obj] + list(extra or [])
+               "-Wno-unused-function", "-Wno-bitwise-instead-of-logical", "-c", "-o", obj] + defs + list(extra or [])
         if src.endswith(".cpp"):
             cmd += ["-x", "hip"]
         cmd.append(os.path.join(CSRC, src))

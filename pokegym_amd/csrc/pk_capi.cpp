@@ -21,6 +21,7 @@
 #include "pk_reward.h"
 
 hipError_t pk_launch_step(const PkStepArgs& a, hipStream_t s);
+hipError_t pk_launch_step_small(const PkStepArgs& a, hipStream_t s);   // pk_step.hip built with PK_K1_SMALL
 hipError_t pk_launch_render(const PkStepArgs& a, hipStream_t s);
 hipError_t pk_launch_reset(const PkResetArgs& a, hipStream_t s);
 hipError_t pk_launch_list(const uint8_t* mask, uint32_t env0, uint32_t env1, uint32_t* cnt, uint32_t* ids, hipStream_t s);
@@ -245,6 +246,11 @@ struct pk_handle {
     int8_t* bank_slot = nullptr;  // [128] LDS slot per ROM bank (-1 = global)
     uint8_t* slot_bank = nullptr; // [PK_LDS_SLOTS]
     uint32_t nslots = 1;
+    // the small-LDS K1 (pk_layout.h): its own slot tables (PK_SMALL_LDS_SLOTS banks)
+    int8_t* bank_slot_s = nullptr;
+    uint8_t* slot_bank_s = nullptr;
+    uint32_t nslots_s = 1;
+    int k1_small = -1;         // PK_K1_SMALL: -1 = for concurrent sub-batch ranges (<= 32 envs per wave), 0 never, 1 always
     size_t lat_stride = 0;
     Template tmpl;
     // reward stack (PK_F_REWARD), see pk_reward.h
@@ -302,7 +308,7 @@ void pk_destroy(pk_handle* h) {
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     void* ptrs[] = {h->mem, h->regs, h->lat, h->screen, h->rom, h->ucode, h->bank_slot, h->slot_bank, h->t_mem, h->t_regs,
                     h->t_lat, h->t_screen, h->scratch, h->rs, h->rsd, h->seen, h->mask, h->cutc, h->obs, h->reload,
-                    h->lists, h->dbg, h->info, h->info_flag, h->heat, h->info_bits};
+                    h->lists, h->dbg, h->info, h->info_flag, h->heat, h->info_bits, h->bank_slot_s, h->slot_bank_s};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete h;
@@ -354,6 +360,7 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
             h->k1_block = (uint32_t)v;
         }
         if (const char* pr = getenv("PK_K1_PRIO")) h->k1_prio = atoi(pr) ? 1 : 0;
+        if (const char* sm = getenv("PK_K1_SMALL")) h->k1_small = atoi(sm) ? 1 : 0;
         // image interleave = K1's envs per wave for this handle (no 64-byte line shared by two
         // waves; a wave's lanes share one sub-block base).  PK_ILV overrides it with any power of
         // two <= 64: narrower than the wave puts one wave's envs in several sub-blocks (K1 reaches
@@ -403,6 +410,8 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     ALLOC(h->ucode, PK_UC_WORDS * 4);
     ALLOC(h->bank_slot, 128);
     ALLOC(h->slot_bank, PK_LDS_SLOTS);
+    ALLOC(h->bank_slot_s, 128);
+    ALLOC(h->slot_bank_s, PK_SMALL_LDS_SLOTS);
     ALLOC(h->t_mem, PK_PHYS);
     ALLOC(h->t_regs, PK_NREGS * 4);
     ALLOC(h->t_lat, 3 * PK_ROWS * 4);
@@ -448,6 +457,11 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
         h->nslots = want;
         if (e == hipSuccess) e = hipMemcpy(h->bank_slot, bs, sizeof bs, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(h->slot_bank, sb, sizeof sb, hipMemcpyHostToDevice);
+        // the small-LDS kernel stages the first PK_SMALL_LDS_SLOTS of the same banks
+        h->nslots_s = want < PK_SMALL_LDS_SLOTS ? want : PK_SMALL_LDS_SLOTS;
+        for (uint32_t k = h->nslots_s; k < want; k++) bs[k] = -1;
+        if (e == hipSuccess) e = hipMemcpy(h->bank_slot_s, bs, sizeof bs, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(h->slot_bank_s, sb, PK_SMALL_LDS_SLOTS, hipMemcpyHostToDevice);
     }
     if (e == hipSuccess) e = hipMemcpy(h->t_mem, h->tmpl.mem.data(), PK_PHYS, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->t_regs, h->tmpl.regs, sizeof h->tmpl.regs, hipMemcpyHostToDevice);
@@ -595,19 +609,34 @@ static uint32_t k1_wave_lanes(const pk_handle* h, uint32_t count) {
 // took every CU and the second range waited: 485k vs 688k env-steps/s).
 // The wide (512-thread) shape puts two waves on each SIMD; those launches take K1's wave-priority
 // variant (measured +5 % at 65,536 envs; with one wave per SIMD it only costs its two instructions).
-static void k1_shape(const pk_handle* h, uint32_t& lanes, uint32_t& block, uint32_t& prio) {
+static void k1_shape(const pk_handle* h, bool small, uint32_t& lanes, uint32_t& block, uint32_t& prio) {
     lanes = k1_wave_lanes(h, h->n);
+    const uint32_t wg_envs = small ? PK_SMALL_WG_ENVS : PK_WG_ENVS;
+    const uint32_t max_threads = small ? PK_SMALL_MAX_THREADS : PK_K1_MAX_THREADS;
     if (h->k1_block) {
-        // PK_K1_BLOCK with the lanes picked for this handle: a workgroup holds at most PK_WG_ENVS
-        // envs (its HRAM code mirror), so a block too large for 64-lane waves is narrowed
-        block = h->k1_block;
-        if ((block / PK_LANES) * lanes > PK_WG_ENVS) block = PK_WG_ENVS / lanes * PK_LANES;
+        // PK_K1_BLOCK with the lanes picked for this handle: a workgroup holds at most wg_envs envs
+        // (its HRAM code mirror), so a block too large for the wave width is narrowed
+        block = h->k1_block < max_threads ? h->k1_block : max_threads;
+        if ((block / PK_LANES) * lanes > wg_envs) block = wg_envs / lanes * PK_LANES;
     } else {
         const uint32_t waves = ((h->n + PK_LANES - 1u) / PK_LANES) * (PK_LANES / lanes);
-        const uint32_t wide = PK_WG_ENVS * PK_LANES / lanes < PK_K1_MAX_THREADS ? PK_WG_ENVS * PK_LANES / lanes : PK_K1_MAX_THREADS;
+        const uint32_t wide = wg_envs * PK_LANES / lanes < max_threads ? wg_envs * PK_LANES / lanes : max_threads;
         block = waves <= h->simds ? 256u : wide;
     }
-    prio = h->k1_prio >= 0 ? (uint32_t)h->k1_prio : (block > 256u ? 1u : 0u);
+    // wave priority pays with two waves of one workgroup per SIMD (measured +5 %); with the small
+    // kernel the SIMD's second wave belongs to the other sub-batch, and priority measured -4 %
+    // (profiles/r04b/summary.txt)
+    prio = h->k1_prio >= 0 ? (uint32_t)h->k1_prio : (block > 256u && !small ? 1u : 0u);
+}
+
+// K1 variant of a launch: the small-LDS kernel for a range smaller than the handle (a VecEnv
+// sub-batch, stepped concurrently with the others on its own stream) while waves carry <= 32 envs
+// (its HRAM mirror holds 128 envs per 256-thread workgroup); measured +3 % on configs[3]'s 32,768-env
+// shard in 2 sub-batches, -3..-7 % for whole-handle launches, which gain nothing from a second
+// workgroup per CU but lose the staged banks (profiles/r04b, r04c)
+static bool k1_small(const pk_handle* h, uint32_t env0, uint32_t env1) {
+    if (h->k1_small >= 0) return h->k1_small != 0 && k1_wave_lanes(h, h->n) <= 32u;
+    return (env1 - env0) < h->n && k1_wave_lanes(h, h->n) <= 32u;
 }
 
 static PkStepArgs step_args(pk_handle* h, const uint8_t* actions, uint32_t env0, uint32_t env1) {
@@ -618,8 +647,12 @@ static PkStepArgs step_args(pk_handle* h, const uint8_t* actions, uint32_t env0,
     a.rom_bank_mask = h->bank_mask; a.mbc = h->mbc; a.frames = h->frames;
     a.release_frame = h->release; a.render_last = (h->flags & PK_F_RENDER) ? 1 : 0;
     a.lat_stride = (uint32_t)h->lat_stride;
-    a.nslots = h->nslots; a.bank_slot = h->bank_slot; a.slot_bank = h->slot_bank;
-    k1_shape(h, a.wave_lanes, a.block, a.prio);
+    const bool small = k1_small(h, env0, env1);
+    a.small = small ? 1u : 0u;
+    a.nslots = small ? h->nslots_s : h->nslots;
+    a.bank_slot = small ? h->bank_slot_s : h->bank_slot;
+    a.slot_bank = small ? h->slot_bank_s : h->slot_bank;
+    k1_shape(h, small, a.wave_lanes, a.block, a.prio);
     a.simds = h->simds;
     a.dbg = h->dbg;
     a.env0 = env0; a.env1 = env1;
@@ -645,7 +678,7 @@ int pk_step_range(pk_handle* h, uint32_t env0, uint32_t count, const uint8_t* ac
     const uint32_t env1 = env0 + count;
     PkStepArgs a = step_args(h, actions, env0, env1);
     if (h->prof && (rc = prof_event(h, s))) return rc;
-    HIPCHK(pk_launch_step(a, s));
+    HIPCHK(a.small ? pk_launch_step_small(a, s) : pk_launch_step(a, s));
     if (h->prof && (rc = prof_event(h, s))) return rc;
     if (a.render_last) HIPCHK(pk_launch_render(a, s));
     if (h->prof && (rc = prof_event(h, s))) return rc;

@@ -83,7 +83,6 @@ enum {
     PK_NREGS
 };
 
-// largest K1 workgroup (one per CU: its envs share one LDS copy of the ROM banks and microcode):
 // diagnostic buffer (-DPK_STAMP phase counters; -DPK_WAVETIME adds one PK_WT_REC-word record per K1 wave)
 #ifdef PK_WAVETIME
 #define PK_WT_REC 6u
@@ -91,7 +90,21 @@ enum {
 #else
 #define PK_DBG_WORDS 64u
 #endif
-// 512 threads = 8 waves, two per SIMD at 221 VGPRs; at most PK_WG_ENVS envs (HRAM code mirror columns)
+
+// K1's LDS budget.  The default kernel stages PK_LDS_SLOTS ROM banks (16 KiB each, slot 0 = bank 0)
+// and the HRAM code mirror of up to PK_WG_ENVS envs: 158 KB, one workgroup per CU, 512 threads =
+// 8 waves, two per SIMD at ~233 VGPRs.  The small-LDS kernel (pk_step.hip compiled a second time
+// with PK_K1_SMALL) stages 2 banks and the mirror of 128 envs in 256-thread workgroups: 78.7 KB, so
+// two workgroups fit on a CU.  pk_capi.cpp launches it for the ranges of concurrent sub-batches
+// (VecEnv), whose workgroups can then start on a CU where the other sub-batch is still in its tail.
+#define PK_SMALL_LDS_SLOTS 2u
+#define PK_SMALL_WG_ENVS 128u
+#define PK_SMALL_MAX_THREADS 256
+#ifdef PK_K1_SMALL
+#define PK_WG_ENVS PK_SMALL_WG_ENVS
+#define PK_LDS_SLOTS PK_SMALL_LDS_SLOTS
+#define PK_K1_MAX_THREADS PK_SMALL_MAX_THREADS
+#endif
 #ifndef PK_K1_MAX_THREADS
 #define PK_K1_MAX_THREADS 512
 #endif
@@ -99,7 +112,7 @@ enum {
 #define PK_WG_ENVS 512u
 #endif
 #ifndef PK_LDS_SLOTS
-#define PK_LDS_SLOTS 6u  // ROM banks (16 KiB each) staged in LDS by the step kernel (slot 0 = bank 0)
+#define PK_LDS_SLOTS 6u
 #endif
 
 // kernel argument blocks (passed by value)
@@ -129,6 +142,7 @@ struct PkStepArgs {
     unsigned long long* dbg;  // diagnostic counters (-DPK_STAMP builds only), else null
     uint32_t env0, env1;      // env range of this launch: [env0, env1), env0 % 64 == 0 (sub-batches)
     uint32_t ilv_sh;          // image interleave: 1 << ilv_sh envs (pk_img_off)
+    uint32_t small;           // launch the small-LDS K1 (pk_launch_step_small)
 };
 
 struct PkResetArgs {

@@ -49,6 +49,11 @@
 #ifndef PK_ITER
 #define PK_ITER(env, ev) ((void)(ev))
 #endif
+// a fast-path RAM-image access (kind 0 read, 1 write) at image offset phys (host simulation:
+// tools/mem_stats.py attributes K1's memory traffic to guest regions)
+#ifndef PK_MEMREF
+#define PK_MEMREF(env, kind, phys) ((void)0)
+#endif
 #ifndef PK_ITER_OP
 #define PK_ITER_OP(env, di) ((void)0)
 #endif
@@ -561,7 +566,11 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
         u32 rm0 = 0, rm1 = 0, om0 = 0, om1 = 0, xm = 0;
         if (rram) {
             rm0 = c.g[o0];
-            if (rd2) rm1 = c.g[o1];
+            PK_MEMREF(c.env, 0u, fast_phys(addr0));
+            if (rd2) {
+                rm1 = c.g[o1];
+                PK_MEMREF(c.env, 0u, fast_phys(addr1));
+            }
         }
         if (rrom) {
             const u32 i0 = rom_lds_index(s, addr0);
@@ -687,9 +696,11 @@ __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc&
             }
         }
         c.g[x.o0] = (u8)x.wv0;
+        PK_MEMREF(env, 1u, fast_phys(x.addr0));
         hcode_st(c, x.addr0, x.wv0);
         if (x.wr2) {
             c.g[x.o1] = (u8)x.wv1;
+            PK_MEMREF(env, 1u, fast_phys(x.addr1));
             hcode_st(c, x.addr1, x.wv1);
         }
     }
@@ -711,8 +722,15 @@ __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc&
 // K1
 // PRIO: the launch runs two waves per SIMD (A.prio, chosen by the host), and K1 raises a wave's
 // issue priority over its dependent fetch -> decode -> operand-read chain (see the prefetch stage)
+#ifdef PK_K1_SMALL
+#define PK_K1_KERNEL pk_step_kernel_small
+#define PK_K1_LAUNCH pk_launch_step_small
+#else
+#define PK_K1_KERNEL pk_step_kernel
+#define PK_K1_LAUNCH pk_launch_step
+#endif
 template <bool PRIO>
-__global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A) {
+__global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) {
     for (u32 i = threadIdx.x; i < PK_UC_WORDS; i += blockDim.x) lds_uc[i] = A.ucode[i];
     for (u32 i = threadIdx.x; i < 128u; i += blockDim.x) lds_slot[i] = A.bank_slot[i];
     for (u32 sl = 0; sl < A.nslots; sl++) {
@@ -1222,9 +1240,10 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) pk_step_kernel(PkStepArgs A
     R[PK_R_RFLAGS * np + env] = s.blank | (s.npend << 8);
 }
 
-hipError_t pk_launch_step(const PkStepArgs& a, hipStream_t s) {
+hipError_t PK_K1_LAUNCH(const PkStepArgs& a, hipStream_t s) {
     // one wave per SIMD while the waves fit, else 512-thread workgroups put two waves on each SIMD
-    // of a CU (the 158 KB of LDS staging allows one workgroup per CU)
+    // of a CU (the 158 KB of LDS staging allows one workgroup per CU; the small-LDS build: 256-thread
+    // workgroups, two per CU)
     const u32 wl = a.wave_lanes;
     const u32 span = ((a.env1 + PK_LANES - 1u) & ~(PK_LANES - 1u)) - a.env0;
     const u32 threads = span * (PK_LANES / wl);
@@ -1232,8 +1251,8 @@ hipError_t pk_launch_step(const PkStepArgs& a, hipStream_t s) {
     const u32 block = a.block ? a.block : (threads / PK_LANES <= a.simds ? 256u : wide);
     const u32 grid = (threads + block - 1) / block;
     if (a.prio)
-        hipLaunchKernelGGL(pk_step_kernel<true>, dim3(grid), dim3(block), 0, s, a);
+        hipLaunchKernelGGL(PK_K1_KERNEL<true>, dim3(grid), dim3(block), 0, s, a);
     else
-        hipLaunchKernelGGL(pk_step_kernel<false>, dim3(grid), dim3(block), 0, s, a);
+        hipLaunchKernelGGL(PK_K1_KERNEL<false>, dim3(grid), dim3(block), 0, s, a);
     return hipGetLastError();
 }

@@ -28,7 +28,8 @@ static void launch_independent(dim3 grid, dim3 block, const std::function<void()
 }
 
 void pk_sim_launch(const char* name, dim3 grid, dim3 block, const std::function<void()>& body) {
-    if (strncmp(name, "pk_step_kernel", 14) != 0) {  // the only kernel with __shared__ + __syncthreads
+    // the only kernel with __shared__ + __syncthreads (pk_step.hip launches it as PK_K1_KERNEL)
+    if (strncmp(name, "pk_step_kernel", 14) != 0 && strncmp(name, "PK_K1_KERNEL", 12) != 0) {
         launch_independent(grid, block, body);
         return;
     }
@@ -95,6 +96,25 @@ extern "C" void pk_sim_iter_op(uint32_t env, uint32_t di) {
     if (!g_iter_on || env >= g_iter_op.size()) return;
     g_iter_op[env].push_back(di);
 }
+// fast-path RAM-image accesses: per env, (iteration << 20) | (kind << 16) | phys (iteration = the
+// env's PK_ITER count so far, so accesses of one wave iteration can be grouped)
+static std::vector<std::vector<uint64_t>> g_mem;
+static bool g_mem_on = false;
+extern "C" void pk_sim_mem_enable(uint32_t n_envs, int on) {
+    g_mem.assign(on ? n_envs : 0, {});
+    g_mem_on = on != 0;
+}
+extern "C" void pk_sim_memref(uint32_t env, uint32_t kind, uint32_t phys) {
+    if (!g_mem_on || env >= g_mem.size()) return;
+    const uint64_t it = env < g_iter.size() ? g_iter[env].size() : 0;
+    g_mem[env].push_back((it << 20) | ((uint64_t)kind << 16) | phys);
+}
+extern "C" uint64_t pk_sim_mem_get(uint32_t env, uint64_t* out, uint64_t cap) {
+    if (env >= g_mem.size()) return 0;
+    uint64_t n = g_mem[env].size();
+    if (out) memcpy(out, g_mem[env].data(), (n < cap ? n : cap) * 8);
+    return n;
+}
 extern "C" uint64_t pk_sim_iter_op_get(uint32_t env, uint32_t* out, uint64_t cap) {
     if (env >= g_iter_op.size()) return 0;
     uint64_t n = g_iter_op[env].size();
@@ -107,3 +127,10 @@ extern "C" uint64_t pk_sim_iter_get(uint32_t env, uint32_t* out, uint64_t cap) {
     if (out) memcpy(out, g_iter[env].data(), (n < cap ? n : cap) * 4);
     return n;
 }
+
+// The small-LDS K1 (pk_step.hip built a second time with PK_K1_SMALL) differs from the default one
+// only in its LDS array sizes; the host simulation runs the default kernel for both launches (with
+// the small kernel's arguments: its 2-bank slot tables and 256-thread workgroups).
+struct PkStepArgs;
+hipError_t pk_launch_step(const PkStepArgs& a, hipStream_t s);
+hipError_t pk_launch_step_small(const PkStepArgs& a, hipStream_t s) { return pk_launch_step(a, s); }

@@ -253,3 +253,27 @@ def test_config4_flow_vs_oracle_per_env():
     for k, t in enumerate(check_at):
         bad = np.nonzero(got_dig[k] != want_dig[k])[0]
         assert not len(bad), f"after step {t + 1}: {len(bad)}/{n} envs differ, first {bad[:8].tolist()}"
+
+
+@pytest.mark.parametrize("lanes", [16, 32])
+def test_small_lds_kernel_48_steps(monkeypatch, lanes):
+    """The small-LDS K1 (pk_step.hip built with PK_K1_SMALL: 2 staged banks, 128-env HRAM mirror,
+    256-thread workgroups, two per CU), forced on a whole-handle launch, over 48 env-steps of pkbench
+    (its banks 2-3 come from the global ROM), 1,024 envs, every env vs the oracle."""
+    import torch
+    from pokegym_amd.emulator import BatchedEmulator
+    from pokegym_amd.testrom.game import game_rom
+    monkeypatch.setenv("PK_K1_SMALL", "1")
+    monkeypatch.setenv("PK_WAVE_LANES", str(lanes))
+    monkeypatch.setenv("PK_K1_BLOCK", "256")
+    rom, n, steps = game_rom(), 1024, 48
+    actions = np.random.default_rng(4800 + lanes).integers(0, 9, (steps, n), dtype=np.uint8)
+    with OP.pool() as ex:
+        futs = OP.batch_digests(ex, rom, None, actions, chunk=64)
+        emu = BatchedEmulator(rom, n, render=True)
+        acts = torch.from_numpy(actions).to(emu.device)
+        for t in range(steps):
+            emu.step(acts[t])
+        torch.cuda.synchronize()
+        _check_states(rom, None, actions, emu, futs, headless=False)
+        emu.close()

@@ -36,9 +36,12 @@ def main():
                 open(os.path.join(td, sub, f), "wb").write(data)
         csrc = os.path.join(td, "pokegym_amd", "csrc")
         objs = []
-        for src in B.SOURCES:
-            obj = os.path.join(td, os.path.splitext(src)[0] + ".o")
-            cmd = [B.HIPCC, f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-fPIC", "-w", "-c", "-o", obj] + extra
+        units = [(src, os.path.splitext(src)[0], []) for src in B.SOURCES]
+        if "PK_K1_SMALL" in open(os.path.join(td, "pokegym_amd", "csrc", "pk_step.hip")).read():
+            units.append(("pk_step.hip", "pk_step_small", ["-DPK_K1_SMALL"]))
+        for src, stem, defs in units:
+            obj = os.path.join(td, stem + ".o")
+            cmd = [B.HIPCC, f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-fPIC", "-w", "-c", "-o", obj] + defs + extra
             if src.endswith(".cpp"):
                 cmd += ["-x", "hip"]
             subprocess.run(cmd + [os.path.join(csrc, src)], check=True)
