@@ -7,15 +7,17 @@ ranks gives `value` = (all ranks' envs * K) / max_elapsed.  Rank 0 prints ONE JS
 
 Workloads (BASELINE.json configs):
   config3 (default at N=1) configs[2]: 65,536 envs/GPU, the last of the 24 frames of every env-step
-          PPU-rendered into a 160x144 u8 screen obs, actions uniform in [0,8) (torch Philox).
+          PPU-rendered into a 160x144 u8 screen obs, actions uniform in [0,8) (torch Philox); stepped
+          through the PufferLib-shaped VecEnv in 2 sub-batches (send/recv, auto-reset).
   config4 (default at N>1) configs[3]: 262,144 envs split over the N GPUs (strong scaling: 131,072
-          per GPU at N=2, 65,536 at N=4, 32,768 at N=8), screen obs, stepped through the
-          PufferLib-shaped VecEnv (send/recv, auto-reset, 2 sub-batches).  At N=1 (--workload config4)
-          and with --envs it runs that many envs per GPU (the configs[3] shard: 32,768).
+          per GPU at N=2, 65,536 at N=4, 32,768 at N=8), screen obs, stepped through VecEnv
+          (send/recv, auto-reset, 2 sub-batches).  At N=1 (--workload config4) and with --envs it runs
+          that many envs per GPU (the configs[3] shard: 32,768).
   config5 configs[4]: config4's shard + the full ram_map reward stack, the (72,80,4) obs, a template
           reload on every done (short episodes, --max-episode-steps, so resets happen in the timed
-          steps) and the RCCL all-reduce of episode statistics every 128 steps.
+          steps) and VecEnv's logging-interval all-reduce of the episode statistics (every 128 steps).
   config2 configs[1]: 4,096 envs on 1 GPU, headless (no PPU), the fixed [0,3,1,2] action cycle.
+  config1 configs[0]'s shape: one drop-in Environment, 1,000 + 10,000 x step(0) (test.py:16-29).
 The ROM is the synthetic game `pkbench` (pokegym_amd/testrom/game.py; --rom-banks 64 for the
 Pokémon-Red-sized 1 MiB variant) because pokemon_red.gb is not shipped; --rom/--state run a real
 cartridge.  Inputs are resident in HBM before the timed region (actions pre-generated on device).
@@ -45,12 +47,13 @@ WORKLOADS = {
                          "1,000 warm-up steps then 10,000 x step(0), as /root/reference/test.py:16-29 times PyBoy+pokegym"),
     "config2": dict(envs=4096, render=False, reward=False, vecenv=False, actions="cycle", bytes=B_HEADLESS,
                     desc="configs[1]: headless (no PPU), RAM-only obs, fixed action cycle [0,3,1,2]"),
-    "config3": dict(envs=65536, render=True, reward=False, vecenv=False, actions="random", bytes=B_SCREEN,
-                    desc="configs[2]: PPU-rendered 160x144 u8 screen obs, random actions"),
+    "config3": dict(envs=65536, render=True, reward=False, vecenv=True, actions="random", bytes=B_SCREEN,
+                    desc="configs[2]: PPU-rendered 160x144 u8 screen obs, random actions, stepped through the "
+                         "PufferLib-shaped VecEnv (send/recv, 2 sub-batches)"),
     "config4": dict(envs=32768, render=True, reward=False, vecenv=True, actions="random", bytes=B_SCREEN,
                     desc="configs[3]: 262,144 envs split over the GPUs (at N=1: its 32,768-env per-GPU shard), "
                          "screen obs, PufferLib-shaped VecEnv send/recv with auto-reset, random actions"),
-    "config5": dict(envs=32768, render=True, reward=True, vecenv=False, actions="random", bytes=B_REWARD,
+    "config5": dict(envs=32768, render=True, reward=True, vecenv=True, actions="random", bytes=B_REWARD,
                     desc="configs[4]: configs[3]'s envs (at N=1 the 32,768-env shard) + full ram_map reward stack + (72,80,4) obs + per-env "
                          "template reload on done + episodic-return all-reduce every 128 steps"),
 }
@@ -168,77 +171,27 @@ def _stamp(workload: str, rom_tag: str):
 class StepFlow:
     """One env-step of the benchmarked workload over every env of this rank (the timed unit).
 
-    VecEnv workloads (configs[3]): one recv/send of each sub-batch, PufferLib's loop (the
-    sub-batches run on their own streams; VecEnv's logging interval does the sticky-error check and
-    the episode-statistics all-reduce).  Reward workloads (configs[4]): step, episodic-return
-    bookkeeping, the per-env template reload on done and, every `log_every` env-steps, the
-    all-reduce of the episode statistics across ranks (RCCL; gloo in the CPU test of this flow,
-    tests/test_dist.py).  Otherwise a plain step.  `timing` records HIP events around the resets
-    and the all-reduces (GPU only)."""
+    VecEnv workloads (configs[2]..[4]): one recv/send of each sub-batch, PufferLib's loop (the
+    sub-batches run on their own streams; finished envs auto-reset on the device — with the reward
+    stack, a template reload — and VecEnv's logging interval does the sticky-error check and the
+    episode/info-statistics all-reduce across ranks: RCCL at N>1, gloo in the CPU test of this flow,
+    tests/test_dist.py).  Otherwise (configs[1]) a plain step of the whole batch."""
 
-    def __init__(self, emu, vec, reward, world, log_every, dev, timing=False, warmup_steps=0):
-        import torch
-        self.emu, self.vec, self.reward, self.world, self.log_every = emu, vec, reward, world, log_every
-        self.dev, self.timing = dev, timing
-        self.ep_ret = torch.zeros(emu.n if vec is None else vec.num_envs, dtype=torch.float64, device=dev)
-        self.stats = torch.zeros(3, dtype=torch.float64, device=dev)  # [sum of episodic returns, episodes, resets]
-        self.rst = []      # (start, end) events around each timed reset
-        self.ar_ev = []    # (start, end) events around each timed all-reduce
-        self.allreduces = 0
-        self.global_stats = None   # the last all-reduced copy of stats (every rank holds the same)
+    def __init__(self, emu, vec, world, log_every, dev):
+        self.emu, self.vec, self.world, self.log_every, self.dev = emu, vec, world, log_every, dev
         self.vec_logs = []         # VecEnv logging-interval records (episode statistics, all-reduced)
 
-    def _ev(self):
-        import torch
-        return torch.cuda.Event(enable_timing=True)
-
     def step(self, t, timed, acts_t=None):
-        import torch
-        import torch.distributed as dist
         acts_t = self.acts[t] if acts_t is None else acts_t
-        if self.vec is not None:
-            vec = self.vec
-            for _ in range(vec.num_batches):
-                obs, rew, term, trunc, infos, ids, masks = vec.recv()
-                if infos:
-                    self.vec_logs.append(infos[0])
-                vec.send(acts_t[vec.current_envs()])
+        if self.vec is None:
+            self.emu.step(acts_t)
             return
-        emu = self.emu
-        obs, rew, term, trunc = emu.step(acts_t)
-        if not self.reward:
-            return
-        d = term.to(torch.float64)
-        self.ep_ret.add_(rew)
-        self.stats[0] += (self.ep_ret * d).sum()
-        self.stats[1] += d.sum()
-        self.ep_ret.mul_(1.0 - d)
-        tm = timed and self.timing
-        if tm:
-            e = (self._ev(), self._ev())
-            e[0].record()
-        emu.reset(term)
-        if tm:
-            e[1].record()
-            self.rst.append(e)
-        if self.world > 1 and t % self.log_every == self.log_every - 1:
-            # configs[4]'s episodic-return all-reduce, every min(128, steps) env-steps
-            if tm:
-                e = (self._ev(), self._ev())
-                e[0].record()
-            glob = self.stats.clone()
-            dist.all_reduce(glob)
-            self.global_stats = glob
-            self.allreduces += 1
-            if tm:
-                e[1].record()
-                self.ar_ev.append(e)
-
-    def reset_ms(self):
-        return sum(a.elapsed_time(b) for a, b in self.rst)
-
-    def allreduce_ms(self):
-        return [a.elapsed_time(b) for a, b in self.ar_ev]
+        vec = self.vec
+        for _ in range(vec.num_batches):
+            obs, rew, term, trunc, infos, ids, masks = vec.recv()
+            if infos:
+                self.vec_logs.append(infos[0])
+            vec.send(acts_t[vec.current_envs()])
 
 
 def run_config1(args):
@@ -398,8 +351,10 @@ def main():
         from pokegym_amd.env import VecEnv
         # logging interval min(128, steps): the episode-stat all-reduce (RCCL at N>1) and the
         # sticky-error check fire inside the timed steps (any `steps` consecutive env-steps hold one)
-        vec = VecEnv(n, rom=rom, state=state, power_on=state is None, device=local, reward=False,
-                     max_episode_steps=max_steps, log_interval=log_every, batch_size=n // args.batches)
+        # with the reward stack (configs[4]): the (72,80,4) obs, a template reload on every done
+        vec = VecEnv(n, rom=rom, state=state, power_on=state is None, device=local, reward=reward,
+                     reload_on_reset=reward, max_episode_steps=max_steps, log_interval=log_every,
+                     batch_size=n // args.batches)
         emu = vec.emu
         vec.async_reset()
     else:
@@ -407,14 +362,13 @@ def main():
                               reload_on_reset=reward, max_episode_steps=max_steps)
         if reward:
             emu.reset()
-    flow = StepFlow(emu, vec, reward, world, log_every, dev, timing=True, warmup_steps=args.warmup + args.steps)
-    stats = flow.stats
+    flow = StepFlow(emu, vec, world, log_every, dev)
     env_step = flow.step
 
     host_copy = None
     if args.host_obs:
         if vec is not None:
-            raise SystemExit("--host-obs: not for the VecEnv workload (its consumer is on the device)")
+            raise SystemExit("--host-obs: not for the VecEnv workloads (their consumer is on the device)")
         src = emu.obs if reward else emu.screen
         dbuf = [torch.empty_like(src) for _ in range(2)]
         hbuf = [torch.empty(src.shape, dtype=src.dtype, pin_memory=True) for _ in range(2)]
@@ -459,7 +413,7 @@ def main():
     if world > 1:
         dist.barrier()
     emu.profile_enable(True)
-    resets0 = float(stats[1].item())
+    logs0 = len(flow.vec_logs)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for t in range(args.warmup, total):
@@ -472,8 +426,7 @@ def main():
     elapsed = time.perf_counter() - t0
     emu_ms, ren_ms, rew_ms, nprof = emu.profile_read()
     instr = emu.last_instr_count()  # last step's emulated instructions (all envs)
-    resets = float(stats[1].item()) - resets0
-    k5_ms, ar_ms = flow.reset_ms(), flow.allreduce_ms()
+    timed_logs = flow.vec_logs[logs0:]   # VecEnv logging records produced inside the timed steps
     # env-steps t (1-based) inside the timed window at which the logging interval fires
     fired = sum(1 for t in range(args.warmup + 1, total + 1) if t % log_every == 0)
     t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -524,11 +477,10 @@ def main():
                              "diagnostic, not the default line)") if args.host_obs else None,
                 "scaling_note": ("the default workload is configs[2] (config3: 65,536 envs on one GPU) at N=1 and "
                                  "configs[3] itself (config4: 262,144 envs split over the N GPUs, strong scaling) at "
-                                 "N>1.  A GPU's rate depends on its env count (config4 through VecEnv, round 3: "
-                                 "32,768 envs ~287k env-steps/s, 65,536 ~433k, 131,072 ~662k, 262,144 ~940k; "
-                                 "profiles/r03) — one launch needs 64 envs per SIMD to hide K1's latency and 128 to "
-                                 "fill every lane — so N=8 (32,768 per GPU) is below 8x the N=1 rate by construction "
-                                 "of configs[3]"),
+                                 "N>1.  A GPU's rate depends on its env count (config4 through VecEnv, round 4: "
+                                 "32,768 envs ~333k env-steps/s, 65,536 ~540k; DESIGN.md section 7) -- one launch "
+                                 "needs 64 envs per SIMD to hide K1's latency and 128 to fill every lane -- so N=8 "
+                                 "(32,768 per GPU) is below 8x the N=1 rate by construction of configs[3]"),
             },
             "roofline": {
                 # what limits K1, measured (PMC issue counts, wave timers): not HBM bandwidth and not
@@ -576,15 +528,13 @@ def main():
                 out["roofline"]["issue"] = stamp["issue"]
         out["collectives"] = {
             "interval_env_steps": log_every,
-            "fired_in_timed_steps": fired if (vec is not None or reward) else 0,
+            "fired_in_timed_steps": len(timed_logs) if vec is not None else 0,
+            "expected_in_timed_steps": fired if vec is not None else 0,
             "what": ("VecEnv logging: sticky-error check + episode/info statistics all-reduce (RCCL at N>1)"
-                     if vec is not None else "episodic-return all-reduce of configs[4] (RCCL at N>1)" if reward else None),
-            "allreduce_ms": [round(x, 3) for x in ar_ms] if ar_ms else None,
+                     if vec is not None else None),
+            "episodes_logged": [round(d.get("episodes", 0.0)) for d in timed_logs] if vec is not None else None,
             "note": None if world > 1 else "one rank: the all-reduce is an identity and is not issued",
         }
-        if reward:
-            out["resets"] = {"envs_reset": int(resets), "k5_reset_ms_total": round(k5_ms, 3),
-                             "k5_reset_ms_per_step": round(k5_ms / max(args.steps, 1), 3)}
         if not args.no_cpu_baseline and world == 1:
             try:
                 out["cpu_baseline"] = _cpu_baseline(rom, state)

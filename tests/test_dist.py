@@ -147,7 +147,7 @@ FLOW_ENVS, FLOW_STEPS, FLOW_LOG = 8, 6, 3
 
 
 def _flow_fn(rank, world, out_dir):
-    """bench.py's StepFlow (the timed per-step unit of configs[3]/[4]) on a host-simulated shard."""
+    """bench.py's StepFlow (the timed per-step unit of configs[2]..[4]) on a host-simulated shard."""
     sys.path.insert(0, os.path.dirname(HERE))
     import bench
     from tests.hostsim.emulator import HostsimEmulator
@@ -155,44 +155,38 @@ def _flow_fn(rank, world, out_dir):
     from pokegym_amd.testrom.game import game_rom
     rom = game_rom()
     acts = torch.from_numpy(np.random.default_rng(7 + rank).integers(0, 8, (FLOW_STEPS, FLOW_ENVS)).astype(np.uint8))
-    # configs[4]: reward stack, template reload on done (2-step episodes), episodic-return all-reduce
-    emu = HostsimEmulator(rom, FLOW_ENVS, reward=True, reload_on_reset=True, max_episode_steps=2)
-    emu.reset()
-    f5 = bench.StepFlow(emu, None, True, world, FLOW_LOG, "cpu")
-    f5.acts = acts
-    for t in range(FLOW_STEPS):
-        f5.step(t, False)
-    local5 = f5.stats.tolist()
-    glob5 = f5.global_stats.tolist()
-    emu.close()
-    # configs[3]: screen-obs VecEnv (PufferLib recv/send, auto-reset), its logging all-reduce
-    emu4 = HostsimEmulator(rom, FLOW_ENVS, render=True, max_episode_steps=2)
-    vec = VecEnv(FLOW_ENVS, emulator=emu4, log_interval=FLOW_LOG, max_episode_steps=2)
-    vec.async_reset()
-    f4 = bench.StepFlow(emu4, vec, False, world, FLOW_LOG, "cpu")
-    f4.acts = acts
-    for t in range(FLOW_STEPS + 1):   # the last logging record is returned by the next recv
-        f4.step(t % FLOW_STEPS, False)
-    logs = [{k: float(v) for k, v in d.items()} for d in f4.vec_logs]
-    vec.close()
+    out = {}
+    # configs[4] (reward stack, template reload on done, 2-step episodes) and configs[3] (screen obs):
+    # VecEnv recv/send with auto-reset, its logging-interval all-reduce
+    for name, kw in (("c5", dict(reward=True, reload_on_reset=True)), ("c4", dict(render=True))):
+        emu = HostsimEmulator(rom, FLOW_ENVS, max_episode_steps=2, **kw)
+        vec = VecEnv(FLOW_ENVS, emulator=emu, log_interval=FLOW_LOG, max_episode_steps=2)
+        vec.async_reset()
+        f = bench.StepFlow(emu, vec, world, FLOW_LOG, "cpu")
+        f.acts = acts
+        for t in range(FLOW_STEPS + 1):   # the last logging record is returned by the next recv
+            f.step(t % FLOW_STEPS, False)
+        out[name] = [{k: (float(v) if not isinstance(v, dict) else {a: float(b) for a, b in v.items()})
+                      for k, v in d.items()} for d in f.vec_logs]
+        vec.close()
     with open(os.path.join(out_dir, f"flow{rank}.txt"), "w") as fh:
-        fh.write(repr({"local5": local5, "glob5": glob5, "allreduces": f5.allreduces, "logs": logs}))
+        fh.write(repr(out))
 
 
 @pytest.mark.slow
 def test_bench_flow_gloo_world2(tmp_path):
-    """bench.py's per-step flow for configs[4] (step, per-env reload on done, episode-statistics
-    all-reduce every FLOW_LOG steps) and configs[3] (VecEnv recv/send with its logging all-reduce)
-    on two gloo ranks, each stepping its own host-simulated shard: the collectives fire inside the
-    run and every rank sees the sum over both shards."""
+    """bench.py's per-step flow for configs[4] (VecEnv with the reward stack: step, per-env template
+    reload on done, episode/info-statistics all-reduce every FLOW_LOG steps) and configs[3] (screen
+    obs) on two gloo ranks, each stepping its own host-simulated shard: the collectives fire inside
+    the run and every rank sees the sum over both shards."""
     mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), _flow_fn), nprocs=2, join=True)
-    got = [eval(open(tmp_path / f"flow{r}.txt").read()) for r in range(2)]
-    assert got[0]["allreduces"] == got[1]["allreduces"] == FLOW_STEPS // FLOW_LOG
-    # the last all-reduce came at the last step: the global stats are the sum of both shards'
-    assert got[0]["glob5"] == got[1]["glob5"] == [a + b for a, b in zip(got[0]["local5"], got[1]["local5"])]
-    assert got[0]["local5"][1] == FLOW_ENVS * (FLOW_STEPS // 2)   # 2-step episodes: every env resets 3 times
-    # VecEnv: two logging records per rank, identical on both ranks (all-reduced); 2-step episodes
-    # end at steps 2 | 4, 6 of the two intervals, on 2 x FLOW_ENVS envs
-    assert len(got[0]["logs"]) == len(got[1]["logs"]) == FLOW_STEPS // FLOW_LOG
-    assert got[0]["logs"] == got[1]["logs"]
-    assert [d["episodes"] for d in got[0]["logs"]] == [2 * FLOW_ENVS * 1, 2 * FLOW_ENVS * 2]
+    got = [eval(open(tmp_path / f"flow{r}.txt").read(), {"nan": float("nan")}) for r in range(2)]
+    for name in ("c5", "c4"):
+        logs = [g[name] for g in got]
+        # two logging records per rank, identical on both ranks (all-reduced); 2-step episodes end at
+        # steps 2 | 4, 6 of the two intervals, on 2 x FLOW_ENVS envs
+        assert len(logs[0]) == len(logs[1]) == FLOW_STEPS // FLOW_LOG
+        assert repr(logs[0]) == repr(logs[1])
+        assert [d["episodes"] for d in logs[0]] == [2 * FLOW_ENVS * 1, 2 * FLOW_ENVS * 2]
+    # the reward flow also all-reduces the info records (one per done)
+    assert [d["info_records"] for d in got[0]["c5"]] == [2 * FLOW_ENVS * 1, 2 * FLOW_ENVS * 2]
