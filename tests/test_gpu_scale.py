@@ -277,3 +277,51 @@ def test_small_lds_kernel_48_steps(monkeypatch, lanes):
         torch.cuda.synchronize()
         _check_states(rom, None, actions, emu, futs, headless=False)
         emu.close()
+
+
+def test_config5_flow_vecenv_vs_oracle_per_env():
+    """The benchmarked configs[4] flow (bench.py config5 since round 4): VecEnv with the reward stack,
+    32,768 envs in 2 sub-batches of 16,384 on their own streams (small-LDS K1, K2, K4, K3 per range),
+    a template reload on every done (pk_reset_range with the reset kernels of the reward stack),
+    max_episode_steps 3 so two resets fire inside 7 steps.  Per env and step, the rewards (exact
+    f64) and dones recv() returns, and the obs of the last step, == the oracle emulator + the reward
+    oracle with reload-on-reset (tests/oracle_pool._reward_run); the sticky error codes VecEnv keeps
+    == the oracle's first error of each env."""
+    import torch
+    import xxhash
+    from pokegym_amd.env import VecEnv
+    from pokegym_amd.testrom.game import game_rom
+    rom, n, steps, max_steps = game_rom(), 32768, 7, 3
+    actions = np.random.default_rng(5327).integers(0, 8, (steps, n), dtype=np.uint8)
+    with OP.pool() as ex:
+        parts = OP.reward_runs_async(ex, rom, None, actions, max_steps, chunk=256)
+        vec = VecEnv(n, rom=rom, power_on=True, reward=True, reload_on_reset=True, max_episode_steps=max_steps,
+                     log_interval=0, batch_size=n // 2)
+        acts = torch.from_numpy(actions).to(vec.device)
+        vec.async_reset()
+        got_rew = np.zeros((steps, n), np.float64)
+        got_done = np.zeros((steps, n), np.uint8)
+        for t in range(steps + 1):
+            for _ in range(vec.num_batches):
+                obs, rew, term, trunc, infos, ids, masks = vec.recv()
+                sl = vec.current_envs()
+                if t > 0:
+                    got_rew[t - 1, sl] = rew.cpu().numpy()
+                    got_done[t - 1, sl] = term.to(torch.uint8).cpu().numpy()
+                vec.send(acts[min(t, steps - 1), sl])   # the extra send's step is not compared
+            if t == steps - 1:
+                vec._join_streams()
+                torch.cuda.synchronize()
+                last_obs = np.array([xxhash.xxh3_64_intdigest(o.tobytes()) for o in vec.emu.obs.cpu().numpy()],
+                                    np.uint64)
+                sticky = vec.sticky_errors.cpu().numpy().copy()
+        torch.cuda.synchronize()
+        vec.close()
+        rew, done, err, obs_d, wram_d = OP.gather_reward_runs(parts, steps, n)
+    live = np.cumsum(err != 0, axis=0) == 0
+    first_err = np.where((err != 0).any(axis=0), err[np.argmax(err != 0, axis=0), np.arange(n)], 0)
+    assert np.array_equal(sticky.astype(np.uint32), first_err.astype(np.uint32))
+    assert np.array_equal(got_rew[live], rew[live]), np.argwhere(got_rew != rew)[:5]
+    assert np.array_equal(got_done[live], done[live]) and done[:, :n // 2].sum() > 0 and done[:, n // 2:].sum() > 0
+    ok = live[-1]
+    assert np.array_equal(last_obs[ok], obs_d[steps][ok])

@@ -12,5 +12,8 @@ PK_BENCH_REHEARSAL=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=
     > $OUT/n2_32768.json 2> $OUT/n2_32768.err && \
 PK_BENCH_REHEARSAL=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
     --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --steps 3 --warmup 1 \
-    > $OUT/n2_default.json 2> $OUT/n2_default.err
+    > $OUT/n2_default.json 2> $OUT/n2_default.err && \
+PK_BENCH_REHEARSAL=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 2 --steps 4 --warmup 1 --workload config5 --envs 16384 \
+    > $OUT/n2_config5.json 2> $OUT/n2_config5.err
 echo "exit=$?" > $OUT/exit.txt
