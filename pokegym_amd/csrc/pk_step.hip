@@ -581,6 +581,7 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
             PK_STAMP_AT(0);
             if (!rd2 & (addr0 >= 0xFF00u) & ((addr0 < 0xFF80u) | (addr0 == 0xFFFFu))) {
                 xm = io_read(c, s, addr0);
+                PK_MEMREF(c.env, 2u, addr0);
                 ev |= PK_EV_RD_IO;
             } else if ((addr0 - 0x4000u < 0x4000u) & pair) {  // unstaged switchable bank: the global ROM
                 const u32 ga = rom_global_index(A, s, addr0);
@@ -709,6 +710,7 @@ __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc&
         St t = s;
         pk_write_slow(&A, c.g, c.lane, c.loc, env, c.gid, &t, x.addr0, x.wv0, x.addr1, x.wv1, x.wr2 ? 1u : 0u,
                       bit(m.U, PK_US_HIFIRST));
+        PK_MEMREF(env, 3u, x.addr0);
         s = t;
         ev |= PK_EV_WR_SLOW;
         PK_STAMP_AT(3);

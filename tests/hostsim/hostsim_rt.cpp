@@ -107,7 +107,7 @@ extern "C" void pk_sim_mem_enable(uint32_t n_envs, int on) {
 extern "C" void pk_sim_memref(uint32_t env, uint32_t kind, uint32_t phys) {
     if (!g_mem_on || env >= g_mem.size()) return;
     const uint64_t it = env < g_iter.size() ? g_iter[env].size() : 0;
-    g_mem[env].push_back((it << 20) | ((uint64_t)kind << 16) | phys);
+    g_mem[env].push_back((it << 20) | ((uint64_t)(kind & 3u) << 16) | (phys & 0xFFFFu));
 }
 extern "C" uint64_t pk_sim_mem_get(uint32_t env, uint64_t* out, uint64_t cap) {
     if (env >= g_mem.size()) return 0;

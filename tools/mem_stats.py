@@ -65,11 +65,14 @@ def main():
     lines_env = Counter()                      # region -> distinct lines per env (summed over envs)
     wave_lines = Counter()                     # region -> sum over wave iterations of distinct lines
     wave_iters = 0
-    recs = {}
+    recs, io_recs = {}, {}
     for e in range(n):
         k = L.pk_sim_mem_get(e, None, 0)
         buf = np.zeros(k, np.uint64)
         L.pk_sim_mem_get(e, buf.ctypes.data, k)
+        io_recs[e] = buf[((buf >> 16) & 3) >= 2]
+        kind_all = ((buf >> 16) & 3).astype(np.int64)
+        buf = buf[kind_all < 2]                      # kinds 2/3: IO reads / slow writes (io_stats below)
         recs[e] = buf
         phys = (buf & 0xFFFF).astype(np.int64)
         kind = ((buf >> 16) & 1).astype(np.int64)
@@ -119,6 +122,26 @@ def main():
         p = pg << 8
         return (0x8000 + p if p < 0x2000 else 0xC000 + p - 0x2000 if p < 0x4000 else 0xFE00 + p - 0x4000 if p < 0x4100
                 else 0xFF00 + p - 0x4100)
+    # IO register reads (io_read) and slow-path writes (IO/MBC/DMA): per wave, the iterations in
+    # which ANY lane takes that path for that address
+    io_w, io_l = Counter(), Counter()
+    for w0 in range(0, n, wl):
+        by_it = defaultdict(set)
+        for e in range(w0, min(n, w0 + wl)):
+            b = io_recs[e]
+            for i, kd, a in zip((b >> 20).astype(np.int64).tolist(), ((b >> 16) & 3).astype(np.int64).tolist(),
+                                (b & 0xFFFF).astype(np.int64).tolist()):
+                by_it[i].add((kd, a))
+                io_l[(kd, a)] += 1
+        for s_ in by_it.values():
+            for ka in s_:
+                io_w[ka] += 1
+        io_w["any"] += len(by_it)
+    nw = (n // wl) * steps
+    print(f"IO paths: wave iterations with any IO read / slow write: {io_w['any'] / nw:.0f} per wave-step")
+    for (kd, a), c in sorted(((k, v) for k, v in io_w.items() if k != "any"), key=lambda kv: -kv[1])[:16]:
+        print(f"  {'read ' if kd == 2 else 'write'} {a:04X}  {c / nw:9.1f} wave-iterations per wave-step, "
+              f"{io_l[(kd, a)] / es:8.1f} per env-step")
     tot = sum(page.values())
     print("top guest pages by wave-iteration line touches:")
     for pg, c in page.most_common(12):
