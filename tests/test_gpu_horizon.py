@@ -15,7 +15,9 @@ so the device is checked over every step of the 10k horizon, each segment a cont
 both sides.  The run is repeated for each K1 launch shape the benchmark uses (SHAPES): the small-
 launch shape (256-thread workgroups, one 32-env wave per SIMD, no wave priority) and the
 benchmarked 512-thread workgroups with the wave-priority kernel, pk_step_kernel<true>, at 16 and
-32 envs per wave (configs[3]/[4]'s 32,768-env shard and configs[2]'s 65,536 envs).
+32 envs per wave (configs[3]/[4]'s 32,768-env shard and configs[2]'s 65,536 envs as whole launches),
+and the small-LDS kernel pk_step_kernel_small at 16 and 32 envs per wave (what the VecEnv sub-batches
+of configs[2]..[4] run since round 4).
 
 test_horizon_65536_envs runs configs[2]'s own launch (65,536 envs) continuously for 240 steps and
 compares one env of every workgroup with the oracle."""
@@ -32,8 +34,12 @@ pytestmark = pytest.mark.gpu
 TOTAL, SEGS, EVERY, NTRAJ = 10000, 8, 250, 64
 SEG = TOTAL // SEGS
 PARTS = SEG // EVERY
-# K1 launch shapes: (PK_WAVE_LANES, PK_K1_BLOCK); (None, None) = what the handle picks for 512 envs
-SHAPES = {"auto": (None, None), "wg512_l16": ("16", "512"), "wg512_l32": ("32", "512")}
+# K1 launch shapes: (PK_WAVE_LANES, PK_K1_BLOCK, PK_K1_SMALL); None = what the handle picks for 512 envs.
+# small_*: the small-LDS kernel the VecEnv sub-batches of configs[2]..[4] run (round 4), forced on
+# the whole 512-env launch in its 256-thread workgroups
+SHAPES = {"auto": (None, None, None), "wg512_l16": ("16", "512", None), "wg512_l32": ("32", "512", None),
+          "small_l16": ("16", "256", "1"), "small_l32": ("32", "256", "1")}
+SHAPE_VARS = ("PK_WAVE_LANES", "PK_K1_BLOCK", "PK_K1_SMALL")
 
 
 def horizon_actions(total=TOTAL, ntraj=NTRAJ) -> np.ndarray:
@@ -45,10 +51,9 @@ def horizon_actions(total=TOTAL, ntraj=NTRAJ) -> np.ndarray:
 
 def _with_shape(shape, fn):
     """Call fn() with the K1 shape environment of `shape` (read by pk_create)."""
-    lanes, block = SHAPES[shape]
-    old = {k: os.environ.get(k) for k in ("PK_WAVE_LANES", "PK_K1_BLOCK")}
+    old = {k: os.environ.get(k) for k in SHAPE_VARS}
     try:
-        for k, v in (("PK_WAVE_LANES", lanes), ("PK_K1_BLOCK", block)):
+        for k, v in zip(SHAPE_VARS, SHAPES[shape]):
             if v is None:
                 os.environ.pop(k, None)
             else:
