@@ -57,7 +57,11 @@ def primary_fusable(op):
     return op not in ctrl
 
 
-def groups(tr, slots, fetch, memw=False):
+MEMR = {0x0A, 0x1A, 0x2A, 0x3A, 0x46, 0x4E, 0x56, 0x5E, 0x66, 0x6E, 0x7E, 0xF0, 0xFA, 0xF2,
+        0x86, 0x8E, 0x96, 0x9E, 0xA6, 0xAE, 0xB6, 0xBE}   # ld r,(rr) / ld a,(hl+-) / ldh / ld a,(nn) / alu a,(hl)
+
+
+def groups(tr, slots, fetch, memw=False, memr=False):
     """tr: list of (pc, op); returns the number of loop iterations"""
     n, i, it = len(tr), 0, 0
     while i < n:
@@ -68,7 +72,7 @@ def groups(tr, slots, fetch, memw=False):
             k = 0
             while k < slots - 1 and j < n:
                 pc2, op2 = tr[j]
-                ok2 = secondary(op2) or (memw and op2 in MEMW and not writes_mem(op))
+                ok2 = secondary(op2) or (memw and op2 in MEMW and not writes_mem(op)) or (memr and op2 in MEMR)
                 if pc2 != (tr[j - 1][0] + ilen(tr[j - 1][1])) & 0xFFFF or not ok2:
                     break
                 if used + ilen(op2) > fetch or pc >= 0x8000:
@@ -113,6 +117,9 @@ def main():
     for slots, fetch in ((1, 4), (2, 4), (3, 4), (2, 8), (3, 8), (4, 8)):
         it = groups(tr, slots, fetch)
         print(f"  slots={slots} fetch={fetch}B: iterations {it}  ({it / max(len(tr), 1):.3f} per instruction)")
+    it = groups(tr, 2, 4, memr=True)
+    print(f"  slots=2 fetch=4B + memory-read secondaries (ld r,(rr) / ldh a,(n) / ld a,(nn) / alu a,(hl)): "
+          f"iterations {it}  ({it / max(len(tr), 1):.3f} per instruction)")
     it = groups(tr, 2, 4, memw=True)
     print(f"  slots=2 fetch=4B + memory-write secondaries (ld (rr),a / ld (hl),r after a non-writing primary): "
           f"iterations {it}  ({it / max(len(tr), 1):.3f} per instruction)")
