@@ -228,13 +228,17 @@ def run_config1(args):
 
     env = Environment(rom_path=rom, state_path=state)
     env.reset()
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
         env.step(0)
+        if (i + 1) % 500 == 0:   # progress on stderr: a long single-env run is otherwise silent for minutes
+            print(f"config1 warm-up {i + 1}/{args.warmup}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     env.emu.profile_enable(True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         env.step(0)
+        if (i + 1) % 500 == 0:
+            print(f"config1 step {i + 1}/{args.steps}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     emu_ms, ren_ms, rew_ms, nprof = env.emu.profile_read()
