@@ -652,6 +652,7 @@ static PkStepArgs step_args(pk_handle* h, const uint8_t* actions, uint32_t env0,
     a.nslots = small ? h->nslots_s : h->nslots;
     a.bank_slot = small ? h->bank_slot_s : h->bank_slot;
     a.slot_bank = small ? h->slot_bank_s : h->slot_bank;
+    a.all_staged = a.nslots >= h->bank_mask + 1u ? 1u : 0u;   // pk_step.hip ALL: no unstaged-bank paths
     k1_shape(h, small, a.wave_lanes, a.block, a.prio);
     a.simds = h->simds;
     a.dbg = h->dbg;

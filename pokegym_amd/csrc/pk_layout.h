@@ -143,6 +143,7 @@ struct PkStepArgs {
     uint32_t env0, env1;      // env range of this launch: [env0, env1), env0 % 64 == 0 (sub-batches)
     uint32_t ilv_sh;          // image interleave: 1 << ilv_sh envs (pk_img_off)
     uint32_t small;           // launch the small-LDS K1 (pk_launch_step_small)
+    uint32_t all_staged;      // every ROM bank is staged in this kernel's LDS slots (the ALL instance)
 };
 
 struct PkResetArgs {

@@ -526,7 +526,7 @@ struct Ex {   // what the rest of the iteration needs from the instruction
     u32 addr0, addr1, o0, o1, wv0, wv1, cycles;
     bool wr, wr2, wram;
 };
-template <bool PRIO>
+template <bool PRIO, bool ALL>
 __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, const Mc& m, u32& ev, Ex& x PK_STAMP_PARAMS) {
     const PkStepArgs& A = *c.A;
     const u32 D = m.D, U = m.U, K = m.K;
@@ -560,7 +560,9 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     {
         const bool rram = rd & fast01;  // addr1 == addr0 for 1-byte reads
         // staged ROM is 16 KB-aligned: inside one block addr1 is staged iff addr0 is, at index + ADIR
-        const bool rrom = rd & rom_staged(s, addr0) & pair;
+        // ALL: every ROM bank is staged in LDS (a cartridge of <= the kernel's slots), so the switchable
+        // bank is staged whatever it is
+        const bool rrom = rd & (ALL ? addr0 < 0x8000u : rom_staged(s, addr0)) & pair;
         // each source has its own result registers, merged by OR below: sharing one register
         // would make the LDS ROM read wait for the image load of other lanes (write-after-write)
         u32 rm0 = 0, rm1 = 0, om0 = 0, om1 = 0, xm = 0;
@@ -731,7 +733,7 @@ __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc&
 #define PK_K1_KERNEL pk_step_kernel
 #define PK_K1_LAUNCH pk_launch_step
 #endif
-template <bool PRIO>
+template <bool PRIO, bool ALL>
 __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) {
     for (u32 i = threadIdx.x; i < PK_UC_WORDS; i += blockDim.x) lds_uc[i] = A.ucode[i];
     for (u32 i = threadIdx.x; i < 128u; i += blockDim.x) lds_slot[i] = A.bank_slot[i];
@@ -926,7 +928,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         const uint4 u2 = ucv2[2u * i2], u2b = ucv2[2u * i2 + 1u];
         // ---------------- execute ----------------
         Ex x;
-        pk_exec<PRIO>(s, c, pc, bytes, m, ev, x PK_STAMP_ARGS);
+        pk_exec<PRIO, ALL>(s, c, pc, bytes, m, ev, x PK_STAMP_ARGS);
         u32 cycles = x.cycles;
         const bool wr = x.wr, wram = x.wram;
         // ---------------- fused secondary op (pk_ucode.h pk_u2_entry) ----------------
@@ -998,7 +1000,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         // global-ROM dwords are requested now, so their latency overlaps the write stage (a lane
         // whose write switches the ROM bank refetches at the top of the next iteration)
         u32 ng0 = 0, ng1 = 0, nga = 0;
-        const bool nfg = !(s.pc < 0x4000u || (s.pc < 0x8000u && s.rb != PK_NO_BANK)) & (s.pc - 0x4000u < 0x3FFEu)
+        const bool nfg = !ALL & !(s.pc < 0x4000u || (s.pc < 0x8000u && s.rb != PK_NO_BANK)) & (s.pc - 0x4000u < 0x3FFEu)
                        & !(s.pc - 0xFF80u < 0x7Du);
         if (nfg) {
             nga = rom_global_index(A, s, s.pc);
@@ -1017,7 +1019,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
         {
             const u32 npc = s.pc;
-            const bool fl = rom_staged(s, npc) && (npc & 0x3FFFu) < 0x3FFEu;
+            const bool fl = (ALL ? npc < 0x8000u : rom_staged(s, npc)) && (npc & 0x3FFFu) < 0x3FFEu;
             // staged ROM or the HRAM code mirror: one LDS byte index, one ds_read2_b32
             const bool fh = npc - 0xFF80u < PK_HC_ROWS - 2u;
             const u32 la = sel(fh, PK_HC_BASE + c.loc * PK_HC_STRIDE + (npc - 0xFF80u), sel(fl, rom_lds_index(s, npc), 0u));
@@ -1252,9 +1254,12 @@ hipError_t PK_K1_LAUNCH(const PkStepArgs& a, hipStream_t s) {
     const u32 wide = PK_WG_ENVS * PK_LANES / wl < PK_K1_MAX_THREADS ? PK_WG_ENVS * PK_LANES / wl : PK_K1_MAX_THREADS;
     const u32 block = a.block ? a.block : (threads / PK_LANES <= a.simds ? 256u : wide);
     const u32 grid = (threads + block - 1) / block;
-    if (a.prio)
-        hipLaunchKernelGGL(PK_K1_KERNEL<true>, dim3(grid), dim3(block), 0, s, a);
-    else
-        hipLaunchKernelGGL(PK_K1_KERNEL<false>, dim3(grid), dim3(block), 0, s, a);
+    if (a.prio) {
+        if (a.all_staged) hipLaunchKernelGGL((PK_K1_KERNEL<true, true>), dim3(grid), dim3(block), 0, s, a);
+        else hipLaunchKernelGGL((PK_K1_KERNEL<true, false>), dim3(grid), dim3(block), 0, s, a);
+    } else {
+        if (a.all_staged) hipLaunchKernelGGL((PK_K1_KERNEL<false, true>), dim3(grid), dim3(block), 0, s, a);
+        else hipLaunchKernelGGL((PK_K1_KERNEL<false, false>), dim3(grid), dim3(block), 0, s, a);
+    }
     return hipGetLastError();
 }

@@ -29,6 +29,7 @@ static void launch_independent(dim3 grid, dim3 block, const std::function<void()
 
 void pk_sim_launch(const char* name, dim3 grid, dim3 block, const std::function<void()>& body) {
     // the only kernel with __shared__ + __syncthreads (pk_step.hip launches it as PK_K1_KERNEL)
+    while (*name == '(') name++;
     if (strncmp(name, "pk_step_kernel", 14) != 0 && strncmp(name, "PK_K1_KERNEL", 12) != 0) {
         launch_independent(grid, block, body);
         return;

@@ -25,8 +25,8 @@ def compile_s(extra, out="/tmp/pk_isa/pk_step.s"):
     return out
 
 
-def kernel_text(lines, prio):
-    name = f"_Z14pk_step_kernelILb{prio}EEv10PkStepArgs:"
+def kernel_text(lines, prio, all_=0):
+    name = f"_Z14pk_step_kernelILb{prio}ELb{all_}EEv10PkStepArgs:"
     start = next(i for i, l in enumerate(lines) if l.startswith(name))
     end = next(i for i in range(start, len(lines)) if lines[i].startswith("; codeLenInByte") or ".Lfunc_end" in lines[i])
     return lines[start:end]
@@ -58,6 +58,7 @@ def classify(ins):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--prio", type=int, default=1)
+    ap.add_argument("--all", type=int, default=0, help="1: the every-bank-staged instance (ALL)")
     ap.add_argument("--s", default=None)
     ap.add_argument("--blocks", action="store_true")
     ap.add_argument("--dump", default=None, help="write the common path's instructions to this file")
@@ -65,7 +66,7 @@ def main():
     a = ap.parse_args()
     path = a.s or compile_s(a.extra)
     lines = open(path).read().splitlines()
-    K = kernel_text(lines, a.prio)
+    K = kernel_text(lines, a.prio, a.all)
     # the outer loop: the "Loop Header: Depth=1" label with the most blocks annotated as its body
     heads = [(i, re.match(r"^\.LBB(\d+_\d+):", l).group(1)) for i, l in enumerate(K) if "Loop Header: Depth=1" in l]
     i0, hb = max(heads, key=lambda h: sum(f"Header=BB{h[1]} Depth=1" in l for l in K))
