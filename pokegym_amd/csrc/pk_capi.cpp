@@ -443,23 +443,47 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
     if (e == hipSuccess) e = hipMemcpy(h->rom, cfg->rom, cfg->rom_len, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->ucode, uc.data(), uc.size() * 4, hipMemcpyHostToDevice);
     {
-        // ROM banks staged in LDS by the step kernel: bank 0 and the first banks after it
-        // (override the count with PK_LDS_SLOTS=1..6 for experiments)
+        // ROM banks staged in LDS by the step kernel: bank 0, then the switchable banks that hold
+        // code or data, in bank order (a bank of one repeated byte — an unused bank of the
+        // cartridge — only after those), so a small slot budget is not spent on an empty bank.
+        // PK_STAGE_BANKS=b1,b2,... puts those banks first (experiments); PK_LDS_SLOTS=1..6 caps the count.
+        const uint32_t nb = banks < 128u ? banks : 128u;   // MBC3: 7-bit bank number
+        std::vector<uint32_t> order;
+        std::vector<bool> used(nb, false);
+        used[0] = true;
+        order.push_back(0);
+        if (const char* ev = getenv("PK_STAGE_BANKS")) {
+            for (const char* q = ev; *q;) {
+                char* end = nullptr;
+                const unsigned long b = strtoul(q, &end, 10);
+                if (end == q) break;
+                if (b < nb && !used[b]) { used[b] = true; order.push_back((uint32_t)b); }
+                q = *end ? end + 1 : end;
+            }
+        }
+        for (int pass = 0; pass < 2; pass++)
+            for (uint32_t b = 1; b < nb; b++) {
+                if (used[b]) continue;
+                const uint8_t* bp = cfg->rom + (size_t)b * 0x4000u;
+                bool blank = true;
+                for (uint32_t i = 1; i < 0x4000u && blank; i++) blank = bp[i] == bp[0];
+                if (blank == (pass == 1)) { used[b] = true; order.push_back(b); }
+            }
         uint32_t want = PK_LDS_SLOTS;
         if (const char* ev = getenv("PK_LDS_SLOTS")) want = (uint32_t)atoi(ev);
         if (want < 1) want = 1;
         if (want > PK_LDS_SLOTS) want = PK_LDS_SLOTS;
-        if (want > banks) want = banks;
+        if (want > nb) want = nb;
         int8_t bs[128];
         uint8_t sb[PK_LDS_SLOTS] = {0};
         memset(bs, -1, sizeof bs);
-        for (uint32_t k = 0; k < want; k++) { sb[k] = (uint8_t)k; bs[k] = (int8_t)k; }
+        for (uint32_t k = 0; k < want; k++) { sb[k] = (uint8_t)order[k]; bs[order[k]] = (int8_t)k; }
         h->nslots = want;
         if (e == hipSuccess) e = hipMemcpy(h->bank_slot, bs, sizeof bs, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(h->slot_bank, sb, sizeof sb, hipMemcpyHostToDevice);
         // the small-LDS kernel stages the first PK_SMALL_LDS_SLOTS of the same banks
         h->nslots_s = want < PK_SMALL_LDS_SLOTS ? want : PK_SMALL_LDS_SLOTS;
-        for (uint32_t k = h->nslots_s; k < want; k++) bs[k] = -1;
+        for (uint32_t k = h->nslots_s; k < want; k++) bs[order[k]] = -1;
         if (e == hipSuccess) e = hipMemcpy(h->bank_slot_s, bs, sizeof bs, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(h->slot_bank_s, sb, PK_SMALL_LDS_SLOTS, hipMemcpyHostToDevice);
     }

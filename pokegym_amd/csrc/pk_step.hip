@@ -127,6 +127,7 @@ struct St {
     u32 mbc;              // rombank | rambank<<8 | ram_enabled<<16 | memorymodel<<24
     u32 misc;             // joypad directional | standard<<8 | (ly_window+1)<<16
     u32 rb;               // LDS byte offset of the switchable ROM bank, PK_NO_BANK = not staged
+    u32 rlim;             // ROM addresses below it are staged: 0x8000, or 0x4000 when rb = PK_NO_BANK
     u32 npend;            // latched, not yet rasterised lines
     u32 render, blank, frame_done;
 };
@@ -159,7 +160,7 @@ __device__ __forceinline__ u32 fast_phys(u32 a) {
 }
 __device__ __forceinline__ bool vram_or_oam(u32 a) { return (a >= 0x8000u && a < 0xA000u) || (a >= 0xFE00u && a < 0xFEA0u); }
 // ROM address staged in LDS?  and its LDS byte index
-__device__ __forceinline__ bool rom_staged(const St& s, u32 a) { return a < 0x4000u || (a < 0x8000u && s.rb != PK_NO_BANK); }
+__device__ __forceinline__ bool rom_staged(const St& s, u32 a) { return a < s.rlim; }
 __device__ __forceinline__ u32 rom_lds_index(const St& s, u32 a) { return sel(a < 0x4000u, a, s.rb + (a & 0x3FFFu)); }
 // byte index in the global ROM of a switchable-bank address (0x4000-0x7FFF)
 __device__ __forceinline__ u32 rom_global_index(const PkStepArgs& A, const St& s, u32 a) {
@@ -287,6 +288,7 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
             v &= 0x7Fu;
             s.mbc = setb8(s.mbc, 0, v == 0u ? 1u : v);
             s.rb = slot_base((s.mbc & 0xFFu) & A.rom_bank_mask);
+            s.rlim = sel(s.rb != PK_NO_BANK, 0x8000u, 0x4000u);
         } else if (a < 0x6000u) {
             s.mbc = setb8(s.mbc, 8, v);
         }
@@ -802,6 +804,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
     s.mbc = R[PK_R_MBC * np + env];
     s.misc = R[PK_R_MISC * np + env];
     s.rb = slot_base((s.mbc & 0xFFu) & A.rom_bank_mask);
+    s.rlim = sel(s.rb != PK_NO_BANK, 0x8000u, 0x4000u);
     s.npend = 0;
     s.blank = 0;
     s.frame_done = 0;
@@ -1000,7 +1003,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         // global-ROM dwords are requested now, so their latency overlaps the write stage (a lane
         // whose write switches the ROM bank refetches at the top of the next iteration)
         u32 ng0 = 0, ng1 = 0, nga = 0;
-        const bool nfg = !ALL & !(s.pc < 0x4000u || (s.pc < 0x8000u && s.rb != PK_NO_BANK)) & (s.pc - 0x4000u < 0x3FFEu)
+        const bool nfg = !ALL & !rom_staged(s, s.pc) & (s.pc - 0x4000u < 0x3FFEu)
                        & !(s.pc - 0xFF80u < 0x7Du);
         if (nfg) {
             nga = rom_global_index(A, s, s.pc);
@@ -1045,9 +1048,16 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         // Common case: a running CPU whose cycles reach neither the next LCD event (nor, LCD off,
         // the frame length), with the timer off and the watchdog budget left — then the whole stage
         // is DIV, clock and watchdog bookkeeping (no interrupt, no latch, no frame end).
+        // The common case's bookkeeping is done for every lane before the test (the rare stage below
+        // works on the advanced clock, DIV and budget; its HALT block undoes and redoes them around
+        // its own cycle count), so the common case is no separate branch with its own copies of them.
         const u32 clk2 = s.clock + cycles;
         const u32 lim = sel(s.lcd0 & 0x80u, s.target, FRAME_CYCLES);
-        if (PK_RARE((s.cpu & CPU_HALT) | (s.tim0 & (4u << 24)) | (clk2 >= lim) | ((int)(cycles + 1u) > slack))) {
+        const bool rare = (s.cpu & CPU_HALT) | (s.tim0 & (4u << 24)) | (clk2 >= lim) | ((int)(cycles + 1u) > slack);
+        s.divacc = (s.divacc + cycles) & 0xFFFFu;
+        s.clock = clk2;
+        slack -= (int)(cycles + 1u);
+        if (PK_RARE(rare)) {
             const u32 tac = s.tim0 >> 24;
             // HALT skip-ahead: a halted CPU that nothing can wake before VBlank (no pending or queued
             // interrupt, timer off, STAT HBlank/OAM/LYC interrupts off, frame not rendered) would spend
@@ -1061,6 +1071,9 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
             if (PK_RARE(s.cpu & CPU_HALT)) {
                 // a halted CPU fast-forwards to the next LCD event and notices pending interrupts only
                 // there, so folded events are observable here: restore the exact event state first
+                s.clock -= cycles;
+                s.divacc = (s.divacc - cycles) & 0xFFFFu;
+                slack += (int)(cycles + 1u);
                 lcd_unfold(s);
                 const u32 cpu = s.cpu, stat = bfe8(s.lcd0, 8), ly = bfe8(s.lcd0, 16), nm = (s.lcd2 >> 24) & 3u;
                 const bool cand = !(cpu & CPU_QUEUED) && ((cpu >> 8) & (cpu >> 16) & 0x1Fu) == 0u
@@ -1104,10 +1117,12 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
                 const int ta = (int)s.target - (int)s.clock;
                 const int mm = ta < tb ? ta : tb;
                 cycles = (u32)(mm < 0 ? 0 : mm);
+                s.clock += cycles;
+                s.divacc = (s.divacc + cycles) & 0xFFFFu;
+                slack -= (int)(cycles + 1u);
                 PK_STAMP_AT(6);
             }
             u32 irq = 0;
-            s.divacc = (s.divacc + cycles) & 0xFFFFu;
             if (PK_RARE(tac & 4u)) {  // TAC enabled (timer.py Timer.tick)
                 const u32 dsh = timer_shift(tac);
                 u32 timac = s.timac + cycles;
@@ -1122,7 +1137,6 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
                 s.tim0 = setb8(s.tim0, 8, tima);
                 s.timac = timac;
             }
-            s.clock += cycles;
             const u32 lcdc = s.lcd0 & 0xFFu;
             const bool lcdev = (lcdc & 0x80u) && s.clock >= s.target;
             if (lcdev) {  // lcd.tick mode transition
@@ -1178,7 +1192,6 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
             }
             s.cpu |= irq << 16;
             PK_STAMP_AT(7);
-            slack -= (int)(cycles + 1u);
             ev |= sel(s.frame_done != 0u || slack < 0, PK_EV_FRAME, 0u);
             if (PK_RARE((s.frame_done != 0u) | (slack < 0))) {  // frame end or watchdog
                 s.frame_done = 0;
@@ -1187,10 +1200,6 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
                 if (frame == A.release_frame && btn != 0xFFu) key_event(s, btn, false);
                 s.render = (A.render_last && frame + 1u == A.frames) ? 1u : 0u;
             }
-        } else {
-            s.divacc = (s.divacc + cycles) & 0xFFFFu;
-            s.clock = clk2;
-            slack -= (int)(cycles + 1u);
         }
         PK_ITER(env, ev);
         PK_ITER_OP(env, sel(exec, sel((bytes & 0xFFu) == 0xCBu, 256u + ((bytes >> 8) & 0xFFu), bytes & 0xFFu),
