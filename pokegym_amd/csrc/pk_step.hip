@@ -569,12 +569,12 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
         // would make the LDS ROM read wait for the image load of other lanes (write-after-write)
         u32 rm0 = 0, rm1 = 0, om0 = 0, om1 = 0, xm = 0;
         if (rram) {
+            // a one-byte read has o1 == o0 (ADIR 0): its second load hits the same line, and m1 is
+            // not taken for it, so the load needs no test of its own
             rm0 = c.g[o0];
+            rm1 = c.g[o1];
             PK_MEMREF(c.env, 0u, fast_phys(addr0));
-            if (rd2) {
-                rm1 = c.g[o1];
-                PK_MEMREF(c.env, 0u, fast_phys(addr1));
-            }
+            if (rd2) PK_MEMREF(c.env, 0u, fast_phys(addr1));
         }
         if (rrom) {
             const u32 i0 = rom_lds_index(s, addr0);
@@ -850,7 +850,14 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         const u32 pend = (cpu0 >> 8) & (cpu0 >> 16) & 0x1Fu;
         bool exec = true, doint = false, dispatch = false;
         u32 pc = s.pc, intflag = 0;
-        if (PK_RARE((cpu0 & (CPU_CRASH | CPU_HALT | CPU_QUEUED)) | pend)) {
+        u32 bytes = pbytes;
+        uint4 e0 = p0, e1 = p1, e2 = p2, e3 = p3;
+        // the three rare stages of the loop top (interrupts / HALT, a fetch that was not prefetched,
+        // a block-copy or LY-poll loop at pc) sit behind one test: the common path pays one branch
+        const bool fe_rare = ((cpu0 & (CPU_CRASH | CPU_HALT | CPU_QUEUED)) | pend) != 0u;
+        const bool loop_at = (pbytes == PK_COPY_W0) | ((pbytes & 0x00FFFFFFu) == PK_POLL_W0);
+        if (PK_RARE(fe_rare | !pf | loop_at)) {
+        if (fe_rare) {
             pf = 0;
             const bool crashed = (cpu0 & CPU_CRASH) != 0u;
             const bool halted = (cpu0 & CPU_HALT) != 0u;
@@ -865,9 +872,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         }
 
         // ---------------- fetch + microcode entry (prefetched, or here when pf = 0) ----------------
-        u32 bytes = pbytes;
-        uint4 e0 = p0, e1 = p1, e2 = p2, e3 = p3;
-        if (PK_RARE(!pf)) {
+        if (!pf) {
             PK_STAMP_AT(8);
             const bool flds = rom_staged(s, pc) && (pc & 0x3FFFu) < 0x3FFEu;
             const u32 la = sel(flds, rom_lds_index(s, pc), 0u);
@@ -907,14 +912,11 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
             e3 = ucv[di * 4u + 3u];
             PK_STAMP_AT(9);
         }
-        icount += sel(exec, 1u, 0u);
-        ev |= sel(exec, PK_EV_EXEC | sel((bytes & 0xFFu) == 0xCBu, PK_EV_CB, 0u), 0u) | sel(pf != 0u, PK_EV_F_LDS, 0u)
-            | sel(dispatch, PK_EV_INT, 0u) | sel(!exec && !dispatch, PK_EV_IDLE, 0u);
-        if (exec) PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, bytes & 0xFFu);
         // ---------------- block copy and LY poll (pk_copy_loop, pk_poll_loop) ----------------
         // whole passes of the loop run here; the iteration then executes the next pass's first
         // instruction as usual (the loop's first bytes identify it: no INT pseudo-op has them)
-        if (PK_RARE((bytes == PK_COPY_W0) | ((bytes & 0x00FFFFFFu) == PK_POLL_W0))) {
+        if ((bytes == PK_COPY_W0) | ((bytes & 0x00FFFFFFu) == PK_POLL_W0)) {
+            if (exec) PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, bytes & 0xFFu);
             if (bytes == PK_COPY_W0) {
                 const u32 k = pk_copy_loop(s, c, pc, slack, icount);
                 if (k) PK_TRACE_SKIP(env, pc, k, 7u);
@@ -923,6 +925,12 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
                 if (k) PK_TRACE_SKIP(env, pc, k, 3u);
             }
         }
+        }
+        icount += sel(exec, 1u, 0u);
+        ev |= sel(exec, PK_EV_EXEC | sel((bytes & 0xFFu) == 0xCBu, PK_EV_CB, 0u), 0u) | sel(pf != 0u, PK_EV_F_LDS, 0u)
+            | sel(dispatch, PK_EV_INT, 0u) | sel(!exec && !dispatch, PK_EV_IDLE, 0u);
+        if (exec && !((bytes == PK_COPY_W0) | ((bytes & 0x00FFFFFFu) == PK_POLL_W0)))
+            PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, bytes & 0xFFu);
         const Mc m = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y, e2.z, e2.w, e3.x, e3.y, e3.z, e3.w};
         const u32 D = m.D;
         // the successor's secondary-op entry (read now: its LDS latency overlaps the execute stage)
