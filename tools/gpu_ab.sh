@@ -21,7 +21,7 @@ if [ -n "$PARITY" ]; then
   n=${LIBS%% *}
   env $(runenv $n) timeout -k 10 600 python -u -m pytest ${PARITY_FILES:-tests/test_gpu_parity.py} -x -q --timeout 200 --timeout-method thread -k "$PARITY" > $O/par_$(tag $n).log 2>&1 || { rc=$?; echo "exit=$rc" > $O/exit.txt; exit $rc; }
 fi
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   for w in $WLS; do
     for n in $LIBS; do
       env $(runenv $n) timeout -k 10 300 python bench.py --steps $STEPS --warmup 2 --no-cpu-baseline --workload $w $BENCH_EXTRA > $O/${w}_$(tag $n)_$rep.json 2>> $O/err.log || { rc=$?; break 3; }
