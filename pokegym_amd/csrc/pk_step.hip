@@ -108,6 +108,11 @@ __shared__ int8_t lds_slot[128];                                                
 __device__ __forceinline__ u32 sel(bool c, u32 a, u32 b) { return c ? a : b; }
 // rare-path hint: the block is laid out away from the hot instruction stream (instruction fetch)
 #define PK_RARE(x) __builtin_expect(!!(x), 0)
+// keep three lane values materialised in VGPRs at this point (an empty asm that reads and
+// rewrites them): stops LLVM from sinking their computation further down the loop body
+#ifndef PK_PIN3
+#define PK_PIN3(a, b, c) asm volatile("" : "+v"(a), "+v"(b), "+v"(c))
+#endif
 // TIMA input clock divider as a shift: TAC & 3 = 0/1/2/3 -> 1024/16/64/256 cycles
 __device__ __forceinline__ u32 timer_shift(u32 tac) { return (0x0806040Au >> (8u * (tac & 3u))) & 0xFFu; }
 __device__ __forceinline__ u32 bit(u32 w, int pos) { return (w >> pos) & 1u; }
@@ -998,6 +1003,10 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
             s.w0 = w0f;
             s.w1 = w1f;
             s.pc = pc2;
+            // materialise the register file here: otherwise LLVM sinks both writebacks (and SP's)
+            // past the next instruction's microcode prefetch, which keeps this entry's selector
+            // registers live there and costs register copies at the loop end
+            PK_PIN3(s.w0, s.w1, s.sp);
             const u32 one = bit(M2, PK_U2B_ONE);
             cycles += ((M2 >> PK_U2B_CYC) & 15u) * 4u + sel(tk2, 4u, 0u);
             slack -= (int)one;

@@ -25,8 +25,9 @@ def compile_s(extra, out="/tmp/pk_isa/pk_step.s"):
     return out
 
 
-def kernel_text(lines, prio, all_=0):
-    name = f"_Z14pk_step_kernelILb{prio}ELb{all_}EEv10PkStepArgs:"
+def kernel_text(lines, prio, all_=0, small=False):
+    name = (f"_Z20pk_step_kernel_smallILb{prio}ELb{all_}EEv10PkStepArgs:" if small
+            else f"_Z14pk_step_kernelILb{prio}ELb{all_}EEv10PkStepArgs:")
     start = next(i for i, l in enumerate(lines) if l.startswith(name))
     end = next(i for i in range(start, len(lines)) if lines[i].startswith("; codeLenInByte") or ".Lfunc_end" in lines[i])
     return lines[start:end]
@@ -59,14 +60,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--prio", type=int, default=1)
     ap.add_argument("--all", type=int, default=0, help="1: the every-bank-staged instance (ALL)")
+    ap.add_argument("--small", action="store_true", help="the small-LDS K1 (compiled with -DPK_K1_SMALL)")
     ap.add_argument("--s", default=None)
     ap.add_argument("--blocks", action="store_true")
     ap.add_argument("--dump", default=None, help="write the common path's instructions to this file")
     ap.add_argument("extra", nargs="*")
     a = ap.parse_args()
-    path = a.s or compile_s(a.extra)
+    path = a.s or compile_s(a.extra + (["-DPK_K1_SMALL"] if a.small else []))
     lines = open(path).read().splitlines()
-    K = kernel_text(lines, a.prio, a.all)
+    K = kernel_text(lines, a.prio, a.all, a.small)
     # the outer loop: the "Loop Header: Depth=1" label with the most blocks annotated as its body
     heads = [(i, re.match(r"^\.LBB(\d+_\d+):", l).group(1)) for i, l in enumerate(K) if "Loop Header: Depth=1" in l]
     i0, hb = max(heads, key=lambda h: sum(f"Header=BB{h[1]} Depth=1" in l for l in K))
