@@ -17,7 +17,9 @@ launch shape (256-thread workgroups, one 32-env wave per SIMD, no wave priority)
 benchmarked 512-thread workgroups with the wave-priority kernel, pk_step_kernel<true>, at 16 and
 32 envs per wave (configs[3]/[4]'s 32,768-env shard and configs[2]'s 65,536 envs as whole launches),
 and the small-LDS kernel pk_step_kernel_small at 16 and 32 envs per wave (what the VecEnv sub-batches
-of configs[2]..[4] run since round 4).
+of configs[2]..[4] run since round 4).  Both K1 instances are covered: the 512-thread shapes stage
+all four pkbench banks (the ALL instance), the small kernel's two slots do not (bank 3 runs from
+the global ROM), and test_horizon_64_bank_rom runs the 6-slot kernel's unstaged-bank instance.
 
 test_horizon_65536_envs runs configs[2]'s own launch (65,536 envs) continuously for 240 steps and
 compares one env of every workgroup with the oracle."""
