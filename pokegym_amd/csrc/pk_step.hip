@@ -962,7 +962,8 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
             // both instructions within the fetched bytes: 4 for ROM code (and inside its 16 KiB bank:
             // the LDS slots of other banks follow it), 3 for code in RAM
             const u32 n2 = (D & 3u) + len2;
-            const bool lenok = sel(pc < 0x8000u, (n2 <= 4u) & ((pc & 0x3FFFu) + n2 <= 0x4000u), n2 <= 3u);
+            const u32 avail = sel(pc < 0x8000u, min(4u, 0x4000u - (pc & 0x3FFFu)), 3u);
+            const bool lenok = n2 <= avail;
             const bool ramok = (pc < 0x8000u) | (!wr & !(pc - 0xFEFEu < 0x82u));
             const u32 lim = sel(s.lcd0 & 0x80u, s.target, FRAME_CYCLES);   // next LCD event / LCD-off frame end
             const bool fuse = (len2 != 0u) & ((int)cycles < slack) & (s.clock + cycles < lim)
