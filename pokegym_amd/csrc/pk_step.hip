@@ -133,6 +133,7 @@ struct St {
     u32 misc;             // joypad directional | standard<<8 | (ly_window+1)<<16
     u32 rb;               // LDS byte offset of the switchable ROM bank, PK_NO_BANK = not staged
     u32 rlim;             // ROM addresses below it are staged: 0x8000, or 0x4000 when rb = PK_NO_BANK
+    u32 lim;              // tick_lim(): clock below it = no LCD event, no LCD-off frame end, timer off
     u32 npend;            // latched, not yet rasterised lines
     u32 render, blank, frame_done;
 };
@@ -170,6 +171,13 @@ __device__ __forceinline__ u32 rom_lds_index(const St& s, u32 a) { return sel(a 
 // byte index in the global ROM of a switchable-bank address (0x4000-0x7FFF)
 __device__ __forceinline__ u32 rom_global_index(const PkStepArgs& A, const St& s, u32 a) {
     return (((s.mbc & 0xFFu) & A.rom_bank_mask) << 14) | (a & 0x3FFFu);
+}
+// The clock the next LCD event (LCD on) or the LCD-off frame end happens at, or 0 while the timer
+// runs: clock + cycles < lim is "the timer/LCD stage has nothing to do" (fused pairs, the common
+// tick).  Kept in St.lim and recomputed wherever target, LCDC or TAC can change: kernel entry and
+// the ends of the rare write and timer/LCD stages.
+__device__ __forceinline__ u32 tick_lim(const St& s) {
+    return sel(s.tim0 & (4u << 24), 0u, sel(s.lcd0 & 0x80u, s.target, FRAME_CYCLES));
 }
 __device__ __forceinline__ u32 slot_base(u32 bank) {
     const int sl = lds_slot[bank & 127u];
@@ -721,6 +729,7 @@ __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc&
                       bit(m.U, PK_US_HIFIRST));
         PK_MEMREF(env, 3u, x.addr0);
         s = t;
+        s.lim = tick_lim(s);
         ev |= PK_EV_WR_SLOW;
         PK_STAMP_AT(3);
     }
@@ -827,6 +836,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
     // (no latch flags to clear for the rendered frame: every consumer of a latched line — K2,
     // flush_lines, K2's blank-screen path — clears its flag)
     s.render = (A.render_last && frame + 1u == A.frames) ? 1u : 0u;
+    s.lim = tick_lim(s);
     const uint4* ucv = reinterpret_cast<const uint4*>(lds_uc);
     const uint4* ucv2 = reinterpret_cast<const uint4*>(lds_uc + PK_UC_U2);
     const u32* romw = reinterpret_cast<const u32*>(lds_rom);
@@ -965,9 +975,9 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
             const u32 avail = sel(pc < 0x8000u, min(4u, 0x4000u - (pc & 0x3FFFu)), 3u);
             const bool lenok = n2 <= avail;
             const bool ramok = (pc < 0x8000u) | (!wr & !(pc - 0xFEFEu < 0x82u));
-            const u32 lim = sel(s.lcd0 & 0x80u, s.target, FRAME_CYCLES);   // next LCD event / LCD-off frame end
-            const bool fuse = (len2 != 0u) & ((int)cycles < slack) & (s.clock + cycles < lim)
-                            & !(s.tim0 & (4u << 24)) & !(wr & !wram) & ramok & lenok;
+            // next LCD event / LCD-off frame end, 0 with the timer on (tick_lim)
+            const bool fuse = (len2 != 0u) & ((int)cycles < slack) & (s.clock + cycles < s.lim)
+                            & !(wr & !wram) & ramok & lenok;
             const u32 M2 = sel(fuse, u2.y, PK_U2_NONE_Y);
             // X (pair, or register in byte 0); Y = register | immediate n, ^ the subtract mask, + delta;
             // one adder X + Y + carry-in (ADC/SBC: F.C; SUB/SBC/CP: ^ 1), a logic unit (AND XOR OR),
@@ -998,8 +1008,8 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
             if (fuse) PK_TRACE(env, s.pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, nxt & 0xFFu);
             ev |= sel(fuse, PK_EV_FUSE, 0u);
 #ifdef PK_DBG_FUSE
-            ev |= sel(len2 != 0u, 1u << 23, 0u) | sel((int)cycles < slack, 1u << 24, 0u) | sel(s.clock + cycles < lim, 1u << 25, 0u)
-                | sel(!(s.tim0 & (4u << 24)), 1u << 26, 0u) | sel(!(wr & !wram) & ramok, 1u << 27, 0u);
+            ev |= sel(len2 != 0u, 1u << 23, 0u) | sel((int)cycles < slack, 1u << 24, 0u) | sel(s.clock + cycles < s.lim, 1u << 25, 0u)
+                | sel(!(wr & !wram) & ramok, 1u << 27, 0u);
 #endif
             s.w0 = w0f;
             s.w1 = w1f;
@@ -1070,8 +1080,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         // works on the advanced clock, DIV and budget; its HALT block undoes and redoes them around
         // its own cycle count), so the common case is no separate branch with its own copies of them.
         const u32 clk2 = s.clock + cycles;
-        const u32 lim = sel(s.lcd0 & 0x80u, s.target, FRAME_CYCLES);
-        const bool rare = (s.cpu & CPU_HALT) | (s.tim0 & (4u << 24)) | (clk2 >= lim) | ((int)(cycles + 1u) > slack);
+        const bool rare = (s.cpu & CPU_HALT) | (clk2 >= s.lim) | ((int)(cycles + 1u) > slack);   // timer on: lim 0
         s.divacc = (s.divacc + cycles) & 0xFFFFu;
         s.clock = clk2;
         slack -= (int)(cycles + 1u);
@@ -1218,6 +1227,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
                 if (frame == A.release_frame && btn != 0xFFu) key_event(s, btn, false);
                 s.render = (A.render_last && frame + 1u == A.frames) ? 1u : 0u;
             }
+            s.lim = tick_lim(s);
         }
         PK_ITER(env, ev);
         PK_ITER_OP(env, sel(exec, sel((bytes & 0xFFu) == 0xCBu, 256u + ((bytes >> 8) & 0xFFu), bytes & 0xFFu),
