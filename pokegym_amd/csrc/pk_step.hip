@@ -133,7 +133,8 @@ struct St {
     u32 misc;             // joypad directional | standard<<8 | (ly_window+1)<<16
     u32 rb;               // LDS byte offset of the switchable ROM bank, PK_NO_BANK = not staged
     u32 rlim;             // ROM addresses below it are staged: 0x8000, or 0x4000 when rb = PK_NO_BANK
-    u32 lim;              // tick_lim(): clock below it = no LCD event, no LCD-off frame end, timer off
+    u32 lim;              // tick_lim(): clock below it = no LCD event, no LCD-off frame end, timer off,
+                          // no frame watchdog
     u32 npend;            // latched, not yet rasterised lines
     u32 render, blank, frame_done;
 };
@@ -174,10 +175,21 @@ __device__ __forceinline__ u32 rom_global_index(const PkStepArgs& A, const St& s
 }
 // The clock the next LCD event (LCD on) or the LCD-off frame end happens at, or 0 while the timer
 // runs: clock + cycles < lim is "the timer/LCD stage has nothing to do" (fused pairs, the common
-// tick).  Kept in St.lim and recomputed wherever target, LCDC or TAC can change: kernel entry and
-// the ends of the rare write and timer/LCD stages.
-__device__ __forceinline__ u32 tick_lim(const St& s) {
-    return sel(s.tim0 & (4u << 24), 0u, sel(s.lcd0 & 0x80u, s.target, FRAME_CYCLES));
+// tick).  Kept in St.lim and recomputed wherever target, LCDC, TAC, the clock or the watchdog
+// budget change outside the common path: kernel entry and the ends of the rare loop-top, write and
+// timer/LCD stages.
+// The frame watchdog fires when cycles + 1 > slack, i.e. clock + cycles >= clock + slack; the
+// common path lowers clock + slack by one per instruction only (cycles move both), and lim is
+// recomputed at least once per frame (every LCD event, the LCD-off frame end), so bounding lim by
+// clock + slack - PK_SLACK_MARGIN (two fused instructions per iteration, at most 70224 / 4 per
+// frame) makes clock + cycles < lim imply the watchdog cannot fire: the common path needs no
+// budget test of its own.  Near the budget's end lim is 0 and every iteration takes the rare stage,
+// which tests the budget exactly.
+#define PK_SLACK_MARGIN (2u * (FRAME_CYCLES / 4u) + 64u)
+__device__ __forceinline__ u32 tick_lim(const St& s, int slack) {
+    const int e = (int)s.clock + slack - (int)PK_SLACK_MARGIN;
+    const u32 lim = sel(s.tim0 & (4u << 24), 0u, sel(s.lcd0 & 0x80u, s.target, FRAME_CYCLES));
+    return min(lim, e > 0 ? (u32)e : 0u);
 }
 __device__ __forceinline__ u32 slot_base(u32 bank) {
     const int sl = lds_slot[bank & 127u];
@@ -698,7 +710,7 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     x.o1 = o1;
 }
 
-__device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc& m, const Ex& x, u32& ev PK_STAMP_PARAMS) {
+__device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc& m, const Ex& x, int slack, u32& ev PK_STAMP_PARAMS) {
     const PkStepArgs& A = *c.A;
     if (x.wram) {
         // VRAM / OAM change while rendered lines are pending: rasterise them first (rare)
@@ -729,7 +741,7 @@ __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc&
                       bit(m.U, PK_US_HIFIRST));
         PK_MEMREF(env, 3u, x.addr0);
         s = t;
-        s.lim = tick_lim(s);
+        s.lim = tick_lim(s, slack);
         ev |= PK_EV_WR_SLOW;
         PK_STAMP_AT(3);
     }
@@ -836,12 +848,12 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
     // (no latch flags to clear for the rendered frame: every consumer of a latched line — K2,
     // flush_lines, K2's blank-screen path — clears its flag)
     s.render = (A.render_last && frame + 1u == A.frames) ? 1u : 0u;
-    s.lim = tick_lim(s);
     const uint4* ucv = reinterpret_cast<const uint4*>(lds_uc);
     const uint4* ucv2 = reinterpret_cast<const uint4*>(lds_uc + PK_UC_U2);
     const u32* romw = reinterpret_cast<const u32*>(lds_rom);
 
     int slack = (int)(16u * FRAME_CYCLES);  // frame watchdog: PK_FRAME_BUDGET - budget (oracle/gbcore.c)
+    s.lim = tick_lim(s, slack);
     // software pipeline: the next instruction's bytes and microcode entry, loaded from LDS at the
     // end of the previous iteration (after its writes, so bank switches and HRAM code stores are
     // seen) while the timer/LCD work runs; pf = 0 -> fetch and decode at the top instead
@@ -940,6 +952,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
                 if (k) PK_TRACE_SKIP(env, pc, k, 3u);
             }
         }
+        s.lim = tick_lim(s, slack);   // the loop fast paths moved the clock and the budget
         }
         icount += sel(exec, 1u, 0u);
         ev |= sel(exec, PK_EV_EXEC | sel((bytes & 0xFFu) == 0xCBu, PK_EV_CB, 0u), 0u) | sel(pf != 0u, PK_EV_F_LDS, 0u)
@@ -976,8 +989,8 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
             const bool lenok = n2 <= avail;
             const bool ramok = (pc < 0x8000u) | (!wr & !(pc - 0xFEFEu < 0x82u));
             // next LCD event / LCD-off frame end, 0 with the timer on (tick_lim)
-            const bool fuse = (len2 != 0u) & ((int)cycles < slack) & (s.clock + cycles < s.lim)
-                            & !(wr & !wram) & ramok & lenok;
+            // (s.lim also bounds the watchdog: clock + cycles < lim implies cycles < slack)
+            const bool fuse = (len2 != 0u) & (s.clock + cycles < s.lim) & !(wr & !wram) & ramok & lenok;
             const u32 M2 = sel(fuse, u2.y, PK_U2_NONE_Y);
             // X (pair, or register in byte 0); Y = register | immediate n, ^ the subtract mask, + delta;
             // one adder X + Y + carry-in (ADC/SBC: F.C; SUB/SBC/CP: ^ 1), a logic unit (AND XOR OR),
@@ -1040,7 +1053,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         }
 
         // ---------------- memory writes (wv0 at addr0, wv1 at addr1) ----------------
-        pk_write(s, c, env, m, x, ev PK_STAMP_ARGS);
+        pk_write(s, c, env, m, x, slack, ev PK_STAMP_ARGS);
 
         // ---------------- prefetch the next instruction (LDS-staged ROM or the HRAM mirror) ----------------
         // wave priority (two waves per SIMD): from here through the next iteration's fetch, decode
@@ -1080,7 +1093,8 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         // works on the advanced clock, DIV and budget; its HALT block undoes and redoes them around
         // its own cycle count), so the common case is no separate branch with its own copies of them.
         const u32 clk2 = s.clock + cycles;
-        const bool rare = (s.cpu & CPU_HALT) | (clk2 >= s.lim) | ((int)(cycles + 1u) > slack);   // timer on: lim 0
+        // timer on: lim 0; the watchdog (cycles + 1 > slack) is within clk2 >= lim (tick_lim)
+        const bool rare = (s.cpu & CPU_HALT) | (clk2 >= s.lim);
         s.divacc = (s.divacc + cycles) & 0xFFFFu;
         s.clock = clk2;
         slack -= (int)(cycles + 1u);
@@ -1227,7 +1241,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
                 if (frame == A.release_frame && btn != 0xFFu) key_event(s, btn, false);
                 s.render = (A.render_last && frame + 1u == A.frames) ? 1u : 0u;
             }
-            s.lim = tick_lim(s);
+            s.lim = tick_lim(s, slack);
         }
         PK_ITER(env, ev);
         PK_ITER_OP(env, sel(exec, sel((bytes & 0xFFu) == 0xCBu, 256u + ((bytes >> 8) & 0xFFu), bytes & 0xFFu),

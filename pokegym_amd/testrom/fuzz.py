@@ -307,3 +307,33 @@ def copydata_rom() -> bytes:
          "copy_a:", "ld a, [hl+]", "ld [de], a", "inc de", "dec bc", "ld a, c", "or b", "jr nz, copy_a", "ret",
          "copy_b:", "ld a, [hl+]", "ld [de], a", "inc de", "dec bc", "ld a, b", "or c", "jr nz, copy_b", "ret"]
     return build_rom("\n".join(L), n_banks=2, title="COPYDATA")
+
+
+def lcd_toggle_rom() -> bytes:
+    """The frame watchdog (oracle/gbcore.c PK_FRAME_BUDGET; K1 folds it into its tick limit): a
+    main loop that switches the LCD on, spins a joypad-dependent count, writes WRAM and switches the
+    LCD off again — faster than once per frame, so the LCD clock restarts and no frame ever ends by
+    itself; every frame is ended by the budget.  A pass whose joypad read shows Select pressed (bit 2
+    low) skips the LCD-off write, and the timer runs in every fourth 256-pass
+    stretch (a TIMA interrupt handler counts), so the budget's end meets LCD events, the timer and
+    interrupts."""
+    L = ["section 0", "org $0040", "reti", "org $0048", "reti",
+         "org $0050", "jp timer_isr",
+         "org $0058", "reti", "org $0060", "reti", "org $0100", "nop", "jp start", "org $0150",
+         "start:", "di", "ld sp, $dff0", "ld a, $04", "ldh [$ff], a", "xor a", "ldh [$06], a", "ei",
+         "ld b, 1",
+         "main:",
+         "ld a, $91", "ldh [$40], a",
+         "ld a, $10", "ldh [$00], a", "ldh a, [$00]", "ldh a, [$00]", "ld d, a", "and $0f", "add a, b", "ld c, a",
+         ".w:", "dec c", "jr nz, .w",
+         "ld a, b", "ld [$c000], a", "ld hl, $c001", "inc [hl]",
+         "ld a, d", "and $04", "jr z, .keep",
+         "xor a", "ldh [$40], a",
+         ".keep:",
+         "inc b", "ld a, b", "and a", "jr nz, main",
+         # every 256 passes: the timer on for one stretch in four
+         "ld hl, $c002", "inc [hl]", "ld a, [hl]", "and $03", "jr nz, .toff",
+         "ld a, $05", "ldh [$07], a", "jp main",
+         ".toff:", "xor a", "ldh [$07], a", "jp main",
+         "timer_isr:", "push af", "ld a, [$c010]", "inc a", "ld [$c010], a", "pop af", "reti"]
+    return build_rom("\n".join(L), n_banks=2, title="LCDTOGGLE")

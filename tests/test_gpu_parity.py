@@ -144,6 +144,18 @@ def test_game_rom_64_banks_parity(render):
     assert not bad, bad
 
 
+def test_frame_watchdog_parity():
+    """Frames ended by the watchdog budget (the LCD switched off faster than once per frame, with
+    timer stretches and TIMA interrupts; fuzz.py lcd_toggle_rom): K1 bounds its tick limit by the
+    budget instead of testing it every iteration, so the budget's end must still land on the
+    oracle's instruction."""
+    from pokegym_amd.testrom.fuzz import lcd_toggle_rom
+    n = 128
+    gpu, ref = _run_both(lcd_toggle_rom(), None, n, 2, 11)
+    bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
+    assert not bad, bad[:4]
+
+
 @pytest.mark.parametrize("shape", [("", ""), ("512", "32"), ("512", "64")])
 def test_hram_code_parity(shape, monkeypatch):
     """Code run from inside, across and outside the HRAM bytes K1 mirrors in LDS (0xFF80-0xFF9F),

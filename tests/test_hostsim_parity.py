@@ -51,6 +51,14 @@ def test_hostsim_hram_code():
     assert check(hram_code_rom(), 8, 3, 5) == []
 
 
+def test_hostsim_frame_watchdog():
+    """The frame watchdog: LCD switched off faster than once per frame (its clock restarts, so
+    frames end on the budget), joypad-dependent passes, timer stretches with TIMA interrupts
+    (pokegym_amd/testrom/fuzz.py lcd_toggle_rom).  K1 folds the budget into its tick limit."""
+    from pokegym_amd.testrom.fuzz import lcd_toggle_rom
+    assert check(lcd_toggle_rom(), 8, 2, 11) == []
+
+
 def test_hostsim_map_load_warp():
     """pkbench's door warp (LCD off for ~5 frames of bulk VRAM/WRAM copies) from the fixture state
     (tests/golden/warp_state.npz, tools/make_golden_warp.py)."""
