@@ -127,7 +127,8 @@ struct St {
     u32 clock, target;    // lcd.clock, lcd.clock_target
     u32 lcd0, lcd1, lcd2; // LCDC|STAT<<8|LY<<16|LYC<<24, SCY|SCX<<8|WY<<16|WX<<24, BGP|OBP0<<8|OBP1<<16|next_mode<<24
     u32 tim0;             // (DIV stale) | TIMA<<8 | TMA<<16 | TAC<<24
-    u32 divacc;           // DIV<<8 | DIV_counter (mod 2^16)
+    u32 divacc;           // DIV<<8 | DIV_counter: its low 16 bits (every reader takes a byte of them, so
+                          // the sums need no mask)
     u32 timac;            // TIMA_counter
     u32 mbc;              // rombank | rambank<<8 | ram_enabled<<16 | memorymodel<<24
     u32 misc;             // joypad directional | standard<<8 | (ly_window+1)<<16
@@ -446,7 +447,7 @@ __device__ __forceinline__ void pk_write_slow(const PkStepArgs* A, u8* g, u32 la
 // advance a running CPU by `cyc` cycles of `ninstr` instructions inside one LCD event window:
 // DIV, clock, watchdog budget (cycles + 1 per instruction) and the instruction count
 __device__ __forceinline__ void pk_skip(St& s, int& slack, u32& icount, u32 cyc, u32 ninstr) {
-    s.divacc = (s.divacc + cyc) & 0xFFFFu;
+    s.divacc += cyc;
     s.clock += cyc;
     slack -= (int)(cyc + ninstr);
     icount += ninstr;
@@ -953,8 +954,9 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
             }
         }
         s.lim = tick_lim(s, slack);   // the loop fast paths moved the clock and the budget
+        icount -= sel(exec, 0u, 1u);   // an interrupt dispatch or idle iteration emulates no instruction
         }
-        icount += sel(exec, 1u, 0u);
+        icount += 1u;   // (the rare loop-top stage takes it back for an interrupt dispatch / idle iteration)
         ev |= sel(exec, PK_EV_EXEC | sel((bytes & 0xFFu) == 0xCBu, PK_EV_CB, 0u), 0u) | sel(pf != 0u, PK_EV_F_LDS, 0u)
             | sel(dispatch, PK_EV_INT, 0u) | sel(!exec && !dispatch, PK_EV_IDLE, 0u);
         if (exec && !((bytes == PK_COPY_W0) | ((bytes & 0x00FFFFFFu) == PK_POLL_W0)))
@@ -1095,7 +1097,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         const u32 clk2 = s.clock + cycles;
         // timer on: lim 0; the watchdog (cycles + 1 > slack) is within clk2 >= lim (tick_lim)
         const bool rare = (s.cpu & CPU_HALT) | (clk2 >= s.lim);
-        s.divacc = (s.divacc + cycles) & 0xFFFFu;
+        s.divacc += cycles;
         s.clock = clk2;
         slack -= (int)(cycles + 1u);
         if (PK_RARE(rare)) {
@@ -1113,7 +1115,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
                 // a halted CPU fast-forwards to the next LCD event and notices pending interrupts only
                 // there, so folded events are observable here: restore the exact event state first
                 s.clock -= cycles;
-                s.divacc = (s.divacc - cycles) & 0xFFFFu;
+                s.divacc -= cycles;
                 slack += (int)(cycles + 1u);
                 lcd_unfold(s);
                 const u32 cpu = s.cpu, stat = bfe8(s.lcd0, 8), ly = bfe8(s.lcd0, 16), nm = (s.lcd2 >> 24) & 3u;
@@ -1145,7 +1147,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
                         s.npend += PK_ROWS - y0;
                     }
                     const u32 skipped = tnew - s.clock;
-                    s.divacc = (s.divacc + skipped) & 0xFFFFu;
+                    s.divacc += skipped;
                     slack -= (int)(skipped + (nev - 1u));
                     s.clock = tnew;
                     s.target = vbl;
@@ -1159,7 +1161,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
                 const int mm = ta < tb ? ta : tb;
                 cycles = (u32)(mm < 0 ? 0 : mm);
                 s.clock += cycles;
-                s.divacc = (s.divacc + cycles) & 0xFFFFu;
+                s.divacc += cycles;
                 slack -= (int)(cycles + 1u);
                 PK_STAMP_AT(6);
             }

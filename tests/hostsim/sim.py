@@ -61,6 +61,11 @@ class SimEmulator:
         if rc:
             raise RuntimeError(lib().pk_last_error().decode())
 
+    def last_instr_count(self) -> int:
+        v = ctypes.c_uint64()
+        lib().pk_last_instr_count(self.h, ctypes.byref(v))
+        return int(v.value)
+
     def snapshot(self, e: int) -> bytes:
         out = np.zeros(142610, np.uint8)
         lib().pk_snapshot(self.h, e, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), len(out))

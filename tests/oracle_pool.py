@@ -171,3 +171,28 @@ def gather_reward_runs(futs, steps: int, n: int):
         for a, r in zip(out, f.result()):
             a[:, e0:e0 + r.shape[1]] = r
     return out
+
+
+def instr_counts(rom, acts):
+    """Per env-step instructions the oracle executes (summed over envs), one gb per env."""
+    import ctypes
+    import numpy as np
+    from oracle import oracle
+    L = oracle.lib()
+    r = np.frombuffer(rom, np.uint8).copy()
+    gs = []
+    for _ in range(acts.shape[1]):
+        g = L.gb_new(r.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), len(r))
+        L.gb_power_on(g)
+        gs.append(g)
+    out = []
+    for t in range(acts.shape[0]):
+        tot = 0
+        for e, g in enumerate(gs):
+            i0 = L.gb_instr_count(g)
+            L.gb_run_action(g, int(acts[t, e]), 24, 8)
+            tot += L.gb_instr_count(g) - i0
+        out.append(tot)
+    for g in gs:
+        L.gb_free(g)
+    return out

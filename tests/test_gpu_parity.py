@@ -144,6 +144,29 @@ def test_game_rom_64_banks_parity(render):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("name", ["game", "lcdtoggle"])
+def test_instr_count_parity(name):
+    """pk_last_instr_count of the gfx950 build == the oracle's executed instructions per env-step
+    (fused pairs, skipped CopyData / LY-poll passes; interrupt dispatch and idle iterations are not
+    instructions), 256 envs of pkbench or the watchdog ROM."""
+    import torch
+    from pokegym_amd.emulator import BatchedEmulator
+    from pokegym_amd.testrom.fuzz import lcd_toggle_rom
+    from pokegym_amd.testrom.game import game_rom
+    from tests import oracle_pool as OP
+    rom = game_rom() if name == "game" else lcd_toggle_rom()
+    n = 256 if name == "game" else 64
+    acts = np.random.default_rng(6).integers(0, 9, size=(3, n), dtype=np.uint8)
+    emu = BatchedEmulator(rom, n, render=True)
+    got = []
+    for t in range(acts.shape[0]):
+        emu.step(torch.from_numpy(acts[t]).to(emu.device))
+        torch.cuda.synchronize()
+        got.append(emu.last_instr_count())
+    emu.close()
+    assert got == OP.instr_counts(rom, acts)
+
+
 def test_frame_watchdog_parity():
     """Frames ended by the watchdog budget (the LCD switched off faster than once per frame, with
     timer stretches and TIMA interrupts; fuzz.py lcd_toggle_rom): K1 bounds its tick limit by the

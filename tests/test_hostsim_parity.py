@@ -8,6 +8,7 @@ import pytest
 
 from pokegym_amd.testrom.fuzz import fuzz_rom
 from pokegym_amd.testrom.game import game_rom
+from tests import oracle_pool as OP
 from tests.hostsim.check import check
 
 STATE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "pokegym_amd", "states",
@@ -57,6 +58,26 @@ def test_hostsim_frame_watchdog():
     (pokegym_amd/testrom/fuzz.py lcd_toggle_rom).  K1 folds the budget into its tick limit."""
     from pokegym_amd.testrom.fuzz import lcd_toggle_rom
     assert check(lcd_toggle_rom(), 8, 2, 11) == []
+
+
+@pytest.mark.parametrize("name", ["game", "fuzz3", "lcdtoggle"])
+def test_hostsim_instr_count(name):
+    """pk_last_instr_count (K1's per-env instruction counter: fused pairs, skipped CopyData / LY-poll
+    passes, interrupt dispatch and idle iterations excluded) == the oracle's executed instructions,
+    step by step."""
+    import numpy as np
+    from pokegym_amd.testrom.fuzz import fuzz_rom, lcd_toggle_rom
+    from pokegym_amd.testrom.game import game_rom
+    from tests.hostsim.sim import SimEmulator
+    rom = {"game": game_rom, "fuzz3": lambda: fuzz_rom(3), "lcdtoggle": lcd_toggle_rom}[name]()
+    acts = np.random.default_rng(5).integers(0, 9, size=(3, 8), dtype=np.uint8)
+    emu = SimEmulator(rom, 8)
+    got = []
+    for t in range(acts.shape[0]):
+        emu.step(acts[t])
+        got.append(emu.last_instr_count())
+    emu.close()
+    assert got == OP.instr_counts(rom, acts)
 
 
 def test_hostsim_map_load_warp():
