@@ -152,19 +152,42 @@ class GB:
         return bool(lib().gb_crashed(self.h))
 
 
-def batch_run(rom: bytes, state: bytes | None, actions: np.ndarray, want_states=True, want_screens=True):
-    """Run n envs x steps env-steps; actions shape (steps, n) uint8. Returns (states, screens)."""
+def threads() -> int:
+    """Oracle threads for a batch: the host's CPU share, at most 16 (the GPU box allots 16 cores to
+    one GPU; os.cpu_count() there shows the whole machine).  PK_ORACLE_PROCS overrides."""
+    return max(1, min(16, os.cpu_count() or 1, int(os.environ.get("PK_ORACLE_PROCS", "16"))))
+
+
+def batch_run(rom: bytes, state: bytes | None, actions: np.ndarray, want_states=True, want_screens=True,
+              nthreads: int | None = None):
+    """Run n envs x steps env-steps; actions shape (steps, n) uint8. Returns (states, screens).
+    Envs are independent, so contiguous env chunks run on threads (ctypes drops the GIL around the
+    re-entrant C call; each chunk clones its own template)."""
     actions = np.ascontiguousarray(actions, dtype=np.uint8)
     steps, n = actions.shape
     r = np.frombuffer(rom, dtype=np.uint8).copy()
     st = np.frombuffer(state, dtype=np.uint8).copy() if state is not None else None
     so = np.zeros((n, STATE_SIZE), np.uint8) if want_states else None
     sc = np.zeros((n, ROWS, COLS), np.uint8) if want_screens else None
-    rc = lib().gb_batch_run(_ptr(r), len(r), _ptr(st) if st is not None else None,
-                            len(st) if st is not None else 0, n, steps, _ptr(actions), 1,
-                            _ptr(so) if so is not None else None, _ptr(sc) if sc is not None else None)
-    if rc:
-        raise ValueError(f"gb_batch_run failed: {rc}")
+    L = lib()
+
+    def run(e0, e1):
+        a = np.ascontiguousarray(actions[:, e0:e1])
+        rc = L.gb_batch_run(_ptr(r), len(r), _ptr(st) if st is not None else None,
+                            len(st) if st is not None else 0, e1 - e0, steps, _ptr(a), 1,
+                            _ptr(so[e0:e1]) if so is not None else None, _ptr(sc[e0:e1]) if sc is not None else None)
+        if rc:
+            raise ValueError(f"gb_batch_run failed: {rc}")
+
+    k = max(1, min(nthreads or threads(), n // 8 or 1))
+    if k == 1:
+        run(0, n)
+    else:
+        from concurrent.futures import ThreadPoolExecutor
+        cuts = [n * i // k for i in range(k + 1)]
+        with ThreadPoolExecutor(k) as ex:
+            for f in [ex.submit(run, cuts[i], cuts[i + 1]) for i in range(k)]:
+                f.result()
     return so, sc
 
 

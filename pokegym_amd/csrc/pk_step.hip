@@ -1307,6 +1307,11 @@ hipError_t PK_K1_LAUNCH(const PkStepArgs& a, hipStream_t s) {
     const u32 wide = PK_WG_ENVS * PK_LANES / wl < PK_K1_MAX_THREADS ? PK_WG_ENVS * PK_LANES / wl : PK_K1_MAX_THREADS;
     const u32 block = a.block ? a.block : (threads / PK_LANES <= a.simds ? 256u : wide);
     const u32 grid = (threads + block - 1) / block;
+    // the shape this build's LDS arrays assume: every env of a workgroup has an HRAM-mirror column
+    // (c.loc < PK_WG_ENVS), whole waves, at most PK_K1_MAX_THREADS threads, staged slots that exist
+    if (wl == 0u || wl > PK_LANES || (wl & (wl - 1u)) || block % PK_LANES || block > PK_K1_MAX_THREADS ||
+        (block / PK_LANES) * wl > PK_WG_ENVS || a.nslots > PK_LDS_SLOTS || (a.env0 % PK_LANES))
+        return hipErrorInvalidValue;
     if (a.prio) {
         if (a.all_staged) hipLaunchKernelGGL((PK_K1_KERNEL<true, true>), dim3(grid), dim3(block), 0, s, a);
         else hipLaunchKernelGGL((PK_K1_KERNEL<true, false>), dim3(grid), dim3(block), 0, s, a);

@@ -234,6 +234,7 @@ class VecEnv:
         self._ready: list[int] = []
         self._current: int | None = None
         self._batch_steps = 0
+        self.logs_fired = 0        # logging intervals that fired (error check + all-reduce issued)
 
     def _range(self, b: int) -> slice:
         return slice(b * self.batch_size, (b + 1) * self.batch_size)
@@ -317,6 +318,7 @@ class VecEnv:
             # stream after these reads again through st.wait_stream(current))
             self._join_streams()
             self.raise_if_failed()
+            self.logs_fired += 1
             infos = [self.stats.allreduce()]
             if self.info_stats is not None:
                 infos[0].update(self.info_stats.allreduce())

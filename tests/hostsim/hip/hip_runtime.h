@@ -73,7 +73,7 @@ static inline void __syncthreads() { pk_sim_barrier->arrive_and_wait(); }
 typedef int hipError_t;
 typedef void* hipStream_t;
 typedef void* hipEvent_t;
-enum { hipSuccess = 0, hipErrorOutOfMemory = 2 };
+enum { hipSuccess = 0, hipErrorInvalidValue = 1, hipErrorOutOfMemory = 2 };
 enum hipMemcpyKind { hipMemcpyHostToDevice, hipMemcpyDeviceToHost, hipMemcpyDeviceToDevice, hipMemcpyHostToHost };
 static inline const char* hipGetErrorString(hipError_t) { return "hostsim error"; }
 static inline hipError_t hipGetLastError() { return hipSuccess; }

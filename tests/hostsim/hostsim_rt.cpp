@@ -128,10 +128,3 @@ extern "C" uint64_t pk_sim_iter_get(uint32_t env, uint32_t* out, uint64_t cap) {
     if (out) memcpy(out, g_iter[env].data(), (n < cap ? n : cap) * 4);
     return n;
 }
-
-// The small-LDS K1 (pk_step.hip built a second time with PK_K1_SMALL) differs from the default one
-// only in its LDS array sizes; the host simulation runs the default kernel for both launches (with
-// the small kernel's arguments: its 2-bank slot tables and 256-thread workgroups).
-struct PkStepArgs;
-hipError_t pk_launch_step(const PkStepArgs& a, hipStream_t s);
-hipError_t pk_launch_step_small(const PkStepArgs& a, hipStream_t s) { return pk_launch_step(a, s); }

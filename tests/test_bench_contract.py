@@ -68,3 +68,9 @@ def test_bench_line_contract():
         assert k in r, k
     assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=1e-2)
     assert 0 < r["k1_ms"] <= r["span_ms"] <= d["ms_per_step"] * 1.05
+    # the per-GPU rate of the whole step (concurrent sub-batch launches together)
+    assert r["achieved_per_step"] == pytest.approx(r["bytes_per_env_step"] * envs / (d["ms_per_step"] / 1e3) / 1e9,
+                                                   rel=0.02)
+    assert r["frac_per_step"] == pytest.approx(r["achieved_per_step"] / r["peak"], rel=1e-2)
+    c = d["collectives"]
+    assert c["fired_in_timed_steps"] == c["expected_in_timed_steps"]

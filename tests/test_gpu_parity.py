@@ -93,9 +93,15 @@ def test_game_rom_parity_wave_shapes(lanes, monkeypatch):
     assert not bad, bad[:4]
 
 
-@pytest.mark.parametrize("seed", [-1, 0, 3, 21, 47])
-@pytest.mark.parametrize("render", [True, False])
-@pytest.mark.parametrize("lanes", ["16", "32", "64"])
+# (lanes, render, seed): seed -1 = pkbench, else a fuzz ROM.  The shapes whole-handle launches take:
+# 32-env waves (65,536-env handles, rendered; the 4,096-env headless config2 handle), 64-env waves
+# (>= 131,072 envs), 16-env waves (32,768-env handles stepped whole); each over pkbench and fuzz ROMs.
+WG512_CASES = [("16", True, -1), ("16", False, 21),
+               ("32", True, -1), ("32", True, 0), ("32", False, 3), ("32", False, -1),
+               ("64", True, 47), ("64", False, -1)]
+
+
+@pytest.mark.parametrize("lanes,render,seed", WG512_CASES)
 def test_fuzz_rom_parity_512_thread_workgroups(seed, render, lanes, monkeypatch):
     """The benchmarked K1 shapes at small n: 512-thread workgroups (PK_K1_BLOCK), 8 waves sharing
     the workgroup's HRAM mirror — 16 envs per wave (configs[3]'s 32,768-env shard: columns up to

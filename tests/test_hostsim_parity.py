@@ -108,3 +108,15 @@ def test_hostsim_copydata_block_path():
     landing inside copies, LCD-off copies (pokegym_amd/testrom/fuzz.py copydata_rom)."""
     from pokegym_amd.testrom.fuzz import copydata_rom
     assert check(copydata_rom(), 16, 4, 7) == []
+
+
+@pytest.mark.parametrize("lanes", ["16", "32"])
+def test_hostsim_small_lds_kernel(lanes, monkeypatch):
+    """The small-LDS K1 (pk_step.hip compiled a second time with PK_K1_SMALL, as build.py does: 2
+    staged banks, the HRAM mirror of 128 envs, 256-thread workgroups) forced on the launch: pkbench's
+    bank 3 from the global ROM, mirror columns up to 127 (128 envs per workgroup at 32 envs per wave)."""
+    monkeypatch.setenv("PK_K1_SMALL", "1")
+    monkeypatch.setenv("PK_WAVE_LANES", lanes)
+    monkeypatch.setenv("PK_K1_BLOCK", "256")
+    assert check(game_rom(), 128, 2, 48 + int(lanes)) == []
+
