@@ -56,6 +56,7 @@ __host__ __device__ static inline uint64_t pk_img_off(uint32_t env, uint32_t phy
 #define PK_P_IO 0x4100u
 #define PK_P_HRAM 0x4180u
 #define PK_P_SRAM 0x4200u
+#define PK_P_UNUSED 0x41FFu   // no guest byte (IE lives in lane regs): K1's dummy store target
 
 #define PK_ROWS 144u
 #define PK_COLS 160u

@@ -113,6 +113,20 @@ __device__ __forceinline__ u32 sel(bool c, u32 a, u32 b) { return c ? a : b; }
 #ifndef PK_PIN3
 #define PK_PIN3(a, b, c) asm volatile("" : "+v"(a), "+v"(b), "+v"(c))
 #endif
+// Drain the vector-memory counter (s_waitcnt vmcnt(0); expcnt/lgkmcnt untouched) at the end of a
+// rare block.  gfx950 counts loads and stores on one in-order counter, and LLVM's wait insertion
+// merges the paths into a loop header conservatively: a load left outstanding on a rare path (the
+// block copy's batch loads past the copy's end, whose stores are skipped) made the common path wait
+// for vmcnt(0) — i.e. for the previous iteration's byte stores — before issuing its operand read,
+// every iteration.  Draining on the rare path keeps the store acknowledgements off the common path.
+#ifndef PK_BF
+#define PK_BF 1      // branch-free image stores in the unstaged-bank instance (pk_write)
+#endif
+#ifndef PK_NO_DRAIN
+#define PK_VM_DRAIN() __builtin_amdgcn_s_waitcnt(0x0F70)
+#else
+#define PK_VM_DRAIN() ((void)0)
+#endif
 // TIMA input clock divider as a shift: TAC & 3 = 0/1/2/3 -> 1024/16/64/256 cycles
 __device__ __forceinline__ u32 timer_shift(u32 tac) { return (0x0806040Au >> (8u * (tac & 3u))) & 0xFFu; }
 __device__ __forceinline__ u32 bit(u32 w, int pos) { return (w >> pos) & 1u; }
@@ -498,6 +512,7 @@ __device__ __forceinline__ u32 pk_copy_loop(St& s, const Ctx& c, u32 pc, int& sl
         for (u32 j = 0; j < 16u; j++)
             if (i0 + j < k) st_img(c, db + i0 + j, b[j]);
     }
+    PK_VM_DRAIN();
     const u32 nbc = (bc - k) & 0xFFFFu;                // >= 1: the loop goes on
     const u32 a = (nbc >> 8) | (nbc & 0xFFu);
     s.w0 = nbc | (((de + k) & 0xFFFFu) << 16);
@@ -711,9 +726,33 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     x.o1 = o1;
 }
 
+// BF (branch-free stores, the unstaged-bank instance): both image stores issue in every iteration,
+// a lane without a plain-RAM write storing to its image's unused byte (phys 0x41FF, pk_layout.h),
+// and the rare write paths drain the memory counter at their end — so the number of memory
+// operations between the next-fetch global-ROM loads (issued before this stage) and their use in
+// the prefetch stage is fixed, and that use waits for those loads alone (vmcnt(2)) instead of for
+// this iteration's store acknowledgements too (vmcnt(0)).
+template <bool BF>
 __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc& m, const Ex& x, int slack, u32& ev PK_STAMP_PARAMS) {
     const PkStepArgs& A = *c.A;
-    if (x.wram) {
+    if constexpr (BF) {
+        if (PK_RARE(x.wram & (s.npend != 0u))) {
+            if (vram_or_oam(x.addr0) | (x.wr2 & vram_or_oam(x.addr1))) {
+                flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.sh, c.glane, env, c.gid);
+                s.npend = 0;
+                ev |= PK_EV_FLUSH;
+            }
+            PK_VM_DRAIN();
+        }
+        const u32 dummy = (PK_P_UNUSED << c.sh) + c.lane;
+        const bool w2 = x.wram & x.wr2;
+        c.g[sel(x.wram, x.o0, dummy)] = (u8)x.wv0;
+        c.g[sel(w2, x.o1, dummy)] = (u8)x.wv1;
+        if (x.wram) PK_MEMREF(env, 1u, fast_phys(x.addr0));
+        if (w2) PK_MEMREF(env, 1u, fast_phys(x.addr1));
+        hcode_st(c, sel(x.wram, x.addr0, 0u), x.wv0);   // address 0: the mirror's dummy row
+        hcode_st(c, sel(w2, x.addr1, 0u), x.wv1);
+    } else if (x.wram) {
         // VRAM / OAM change while rendered lines are pending: rasterise them first (rare)
         // (lines are pending only in the rendered frame: test that first, alone)
         if (PK_RARE(s.npend != 0u)) {
@@ -745,6 +784,7 @@ __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc&
         s.lim = tick_lim(s, slack);
         ev |= PK_EV_WR_SLOW;
         PK_STAMP_AT(3);
+        if constexpr (BF) PK_VM_DRAIN();
     }
     ev |= sel(x.wr, PK_EV_WR | sel(x.wr2, PK_EV_WR2, 0u) | sel(x.addr0 >= 0xFF80u && x.addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
                         | sel(x.addr0 >= 0xC000u && x.addr0 < 0xFE00u, PK_EV_WR_WRAM,
@@ -1055,7 +1095,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         }
 
         // ---------------- memory writes (wv0 at addr0, wv1 at addr1) ----------------
-        pk_write(s, c, env, m, x, slack, ev PK_STAMP_ARGS);
+        pk_write<PK_BF && !ALL>(s, c, env, m, x, slack, ev PK_STAMP_ARGS);
 
         // ---------------- prefetch the next instruction (LDS-staged ROM or the HRAM mirror) ----------------
         // wave priority (two waves per SIMD): from here through the next iteration's fetch, decode
