@@ -18,4 +18,6 @@ $B --no-cpu-baseline --workload config4 --rom-banks 64 > $OUT/config4_b64.json 2
 $B --no-cpu-baseline --workload config4 --envs 65536 --steps 10 > $OUT/config4_n65536.json 2>> $OUT/err.log && \
 $B --no-cpu-baseline --workload config4 --envs 131072 --steps 8 > $OUT/config4_n131072.json 2>> $OUT/err.log && \
 $B --no-cpu-baseline --workload config4 --envs 262144 --steps 4 --warmup 1 > $OUT/config4_n262144.json 2>> $OUT/err.log
-echo "exit=$?" > $OUT/exit.txt
+rc=$?
+echo "exit=$rc" > $OUT/exit.txt
+exit $rc

@@ -29,3 +29,4 @@ for spec in "$@"; do
       python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline $args > $D/issue_bench.json 2> $D/issue.err || { rc=$?; break; }
 done
 echo "exit=$rc" > $OUT/exit.txt
+exit $rc
