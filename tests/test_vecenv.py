@@ -169,3 +169,26 @@ def test_vecenv_padded_sub_batch_slots(monkeypatch):
         assert torch.equal(r, ids.to(torch.float64)) and torch.equal(o[:, 0, 0, 0], ids.to(torch.uint8))
         env.send(ids.to(torch.uint8))
     assert (emu.stepped[pad] == 0).all()
+
+
+def test_vecenv_logging_interval_counted_where_it_fires(monkeypatch):
+    """The sub-batch pipeline's logging interval (sticky-error check + statistics all-reduce) fires
+    on the send that completes every log_interval-th env-step; VecEnv.logs_fired counts it there,
+    while its record reaches the caller only with the next recv() (bench.py reports both)."""
+    for name in ("Stream", "Event", "current_stream", "stream"):
+        monkeypatch.setattr(torch.cuda, name, _NoStream)
+    monkeypatch.setattr(torch.Tensor, "record_stream", lambda self, s: None)
+    emu = FakeRangeEmu(128, done_every=1000)
+    env = VecEnv(128, emulator=emu, batch_size=64, log_interval=3)
+    env.async_reset()
+    got = []
+    for t in range(1, 7):                       # env-steps 1..6: the interval fires at 3 and 6
+        for _ in range(env.num_batches):
+            o, r, d, tr, infos, ids, m = env.recv()
+            got.append((t, len(infos)))
+            env.send(torch.zeros(64, dtype=torch.uint8))
+        assert env.logs_fired == t // 3
+    # records handed out: by the first recv after the interval's last send (env-step 4's), not at 6
+    assert [t for t, k in got if k] == [4]
+    o, r, d, tr, infos, ids, m = env.recv()
+    assert len(infos) == 1                     # the interval that fired at env-step 6
