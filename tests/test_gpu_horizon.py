@@ -4,19 +4,19 @@ BASELINE.json's north_star asks for bit-exact WRAM over 10k scripted steps, and 
 only benchmark is 10,000 x step(0) (/root/reference/test.py:16-29).  Timing bugs (DIV-mixing RNG,
 folded LCD events, HALT skip-ahead, fused instruction pairs) grow with the horizon, so this
 compares the WHOLE machine state (v9 savestate digest: WRAM, VRAM, OAM, HRAM, IO, CPU/LCD/timer/
-MBC registers, clocks, the rendered screen) every 125 env-steps along 64 trajectories of 10,000
+MBC registers, clocks, the rendered screen) every 100 env-steps along 64 trajectories of 10,000
 steps each from power-on: trajectory 0 presses Down every step (test.py's a_t = 0), trajectory 1
 the [0,3,1,2] cycle of configs[1], trajectories 2..63 seeded random presses 0..8 (8 = no button).
 
-The 10,000 steps of a trajectory are split into 16 segments of 625 that run side by side in one
-1,024-env launch: segment k starts from the oracle's own v9 state at step 625k (pk_load_env) —
+The 10,000 steps of a trajectory are split into 20 segments of 500 that run side by side in one
+1,280-env launch: segment k starts from the oracle's own v9 state at step 500k (pk_load_env) —
 so the device is checked over every step of the 10k horizon, each segment a continuous run of
-625 device steps, while the wall time is that of 625 steps.  Segment 0 starts from power-on on
-both sides; the whole state is compared every 125 steps.  The run is repeated for each K1 launch
+500 device steps, while the wall time is that of 500 steps.  Segment 0 starts from power-on on
+both sides; the whole state is compared every 100 steps.  The run is repeated for each K1 launch
 shape the benchmark launches (SHAPES): the small-LDS kernel pk_step_kernel_small at 32 and 16 envs
 per wave (what the VecEnv sub-batches of configs[2] and configs[3]/[4] run) and the 512-thread
 workgroups with the wave-priority kernel, pk_step_kernel<true>, at 32 envs per wave (whole-handle
-launches), and the auto-picked shape of a 1,024-env handle, which is configs[1]'s 4,096-env launch
+launches), and the auto-picked shape of a 1,280-env handle, which is configs[1]'s 4,096-env launch
 (256-thread workgroups, one 32-env wave per SIMD).  Both K1 instances are covered: the 512-thread shape stages all four pkbench banks (the
 ALL instance), the small kernel's two slots do not (bank 3 runs from the global ROM), and
 test_horizon_64_bank_rom runs the 6-slot kernel's unstaged-bank instance.  PK_HORIZON_EXTENDED=1
@@ -35,13 +35,13 @@ from tests import oracle_pool as OP
 
 pytestmark = pytest.mark.gpu
 
-TOTAL, SEGS, EVERY, NTRAJ = 10000, 16, 125, 64
+TOTAL, SEGS, EVERY, NTRAJ = 10000, 20, 100, 64
 SEG = TOTAL // SEGS
 PARTS = SEG // EVERY
 # K1 launch shapes: (PK_WAVE_LANES, PK_K1_BLOCK, PK_K1_SMALL); None = what the handle picks.
 # small_*: the small-LDS kernel the VecEnv sub-batches of configs[2]..[4] run (round 4), forced on
-# the whole 1,024-env launch in its 256-thread workgroups
-# "auto" at 1,024 envs is configs[1]'s launch (4,096-env handles: 256-thread workgroups, one 32-env
+# the whole 1,280-env launch in its 256-thread workgroups
+# "auto" at 1,280 envs is configs[1]'s launch (4,096-env handles: 256-thread workgroups, one 32-env
 # wave per SIMD, no priority).
 SHAPES = {"small_l32": ("32", "256", "1"), "small_l16": ("16", "256", "1"), "wg512_l32": ("32", "512", None),
           "auto": (None, None, None)}
@@ -159,13 +159,13 @@ def test_horizon_65536_envs():
 
 def test_horizon_64_bank_rom():
     """The 1 MiB pkbench layout (overworld engine in 60 unstaged switchable banks: global-ROM fetch
-    and reads, Bankswitch every frame) over 2,000 scripted steps: 64 trajectories in 8 segments of
-    250 steps run side by side, whole v9 state compared with the oracle at every segment end."""
+    and reads, Bankswitch every frame) over 2,000 scripted steps: 64 trajectories in 16 segments of
+    125 steps run side by side, whole v9 state compared with the oracle at every segment end."""
     import torch
     from pokegym_amd.emulator import BatchedEmulator
     from pokegym_amd.testrom.game import game_rom
     rom = game_rom(64)
-    total, segs, ntraj = 2000, 8, 64
+    total, segs, ntraj = 2000, 16, 64
     seg = total // segs
     actions = horizon_actions(total, ntraj)
     with OP.pool() as ex:
