@@ -27,6 +27,7 @@
 #define __builtin_amdgcn_readfirstlane(x) (x)
 #define __builtin_amdgcn_s_setprio(x) ((void)0)
 #define __builtin_amdgcn_s_waitcnt(x) ((void)0)
+#define __builtin_nontemporal_store(v, p) (*(p) = (v))
 #define PK_PIN3(a, b, c) ((void)0)
 // lanes run one at a time: a ballot of this lane alone (uses test ballot(x) != 0 for "any lane")
 #define __builtin_amdgcn_ballot_w64(x) ((uint64_t)(bool)(x))
