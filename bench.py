@@ -500,14 +500,16 @@ def main():
                 # MFMA; `peak`/`frac` price the algorithmic bytes against the HBM roofline
                 "bound": "latency",
                 "priced_against": "hbm",
-                "measured_bound": ("dependent latency + issue (not HBM, not MFMA): per loop iteration (one emulated "
-                                   "SM83 instruction, two when a register-only successor fuses) a wave runs the LDS "
-                                   "fetch -> microcode -> address -> operand-read chain of its divergent lanes and the "
-                                   "fused datapath; with two waves per SIMD the chain dominates, with one converged "
-                                   "wave (config2) issue does; a launch lasts as long as its slowest wave (an env in a "
-                                   "long LCD-off map load: kernel ~1.35x the mean wave, profiles/r03_wavetime, "
-                                   "profiles/r03_ab/lypoll).  `issue` carries the PMC ISA counts per emulated "
-                                   "instruction; `frac` is only the HBM price of the algorithmic bytes (DESIGN.md §5)"),
+                "measured_bound": ("instruction issue + dependent latency (not HBM, not MFMA): per loop iteration (one "
+                                   "emulated SM83 instruction, two when a register-only successor fuses) a wave runs the "
+                                   "LDS fetch -> microcode -> address -> operand-read chain of its divergent lanes and the "
+                                   "fused datapath; with two waves per SIMD the SIMD's other wave covers the chain's "
+                                   "latency (requesting the operand ~50 instructions earlier saved nothing, "
+                                   "profiles/r05/ab_pre), so instruction cuts are what move the rate; a lone wave "
+                                   "(config2) is ~70 % issue; a launch lasts as long as its slowest wave (an env in a "
+                                   "long LCD-off map load: kernel ~1.35x the mean wave, profiles/r03_wavetime).  `issue` "
+                                   "carries the PMC ISA counts per emulated instruction; `frac` is only the HBM price of "
+                                   "the algorithmic bytes (DESIGN.md §5)"),
                 "kernel": ("pk_step_kernel (K1, 24 emulated frames) + pk_render_kernel (K2)"
                            + (" + pk_reward_kernel/pk_obs_kernel (K4/K3)" if reward else "")),
                 "span": ("sum of the step's kernel times per launch (HIP events on the launch stream, averaged "
