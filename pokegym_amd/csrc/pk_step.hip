@@ -33,6 +33,10 @@
 #define CPU_HALT 2u
 #define CPU_QUEUED 4u
 #define CPU_CRASH 8u
+// kernel-internal: IE & IF & 0x1F != 0 (an interrupt is pending), kept in step by cpu_sync_pend
+// wherever IE or IF change (all on rare paths) and cleared before the word is stored, so the loop
+// top's rare test is one mask test of the word
+#define CPU_PEND 0x20u
 #define PK_NO_BANK 0xFFFFFFFFu
 
 
@@ -106,12 +110,19 @@ __shared__ int8_t lds_slot[128];                                                
 // ---------------------------------------------------------------------------------------------
 // branch-free helpers: arguments are evaluated unconditionally, so ?: on them is a v_cndmask
 __device__ __forceinline__ u32 sel(bool c, u32 a, u32 b) { return c ? a : b; }
+__device__ __forceinline__ u32 cpu_sync_pend(u32 cpu) {
+    return (cpu & ~CPU_PEND) | sel(((cpu >> 8) & (cpu >> 16) & 0x1Fu) != 0u, CPU_PEND, 0u);
+}
 // rare-path hint: the block is laid out away from the hot instruction stream (instruction fetch)
 #define PK_RARE(x) __builtin_expect(!!(x), 0)
 // keep three lane values materialised in VGPRs at this point (an empty asm that reads and
 // rewrites them): stops LLVM from sinking their computation further down the loop body
 #ifndef PK_PIN3
 #define PK_PIN3(a, b, c) asm volatile("" : "+v"(a), "+v"(b), "+v"(c))
+#endif
+// make a lane value opaque to LLVM at this point (an empty asm that rewrites it in place)
+#ifndef PK_OPAQUE
+#define PK_OPAQUE(x) asm("" : "+v"(x))
 #endif
 // Drain the vector-memory counter (s_waitcnt vmcnt(0); expcnt/lgkmcnt untouched) at the end of a
 // rare block.  gfx950 counts loads and stores on one in-order counter, and LLVM's wait insertion
@@ -132,6 +143,21 @@ __device__ __forceinline__ u32 timer_shift(u32 tac) { return (0x0806040Au >> (8u
 __device__ __forceinline__ u32 bit(u32 w, int pos) { return (w >> pos) & 1u; }
 __device__ __forceinline__ int sfield(u32 w, int pos, int bits) { return ((int)(w << (32 - pos - bits))) >> (32 - bits); }
 __device__ __forceinline__ u32 perm(u32 hi, u32 lo, u32 s) { return __builtin_amdgcn_perm(hi, lo, s); }
+// Lane selects on a microcode bit as masks: bmask = all ones / all zeros from bit pos of w (one
+// v_bfe_i32), msel = m ? a : b for such a mask (one v_bfi_b32 / v_bitop3_b32) — one VALU less per
+// condition than a compare into a lane mask + v_cndmask.  The empty asm keeps the mask opaque:
+// LLVM would otherwise see a sign-extended bit and turn msel back into compare + select.
+__device__ __forceinline__ u32 bmask(u32 w, int pos) {
+    u32 m = (u32)((int)(w << (31 - pos)) >> 31);
+    PK_OPAQUE(m);
+    return m;
+}
+__device__ __forceinline__ u32 msel(u32 m, u32 a, u32 b) { return (a & m) | (b & ~m); }
+// The initial value of a register that a divergent branch writes and that lanes outside the
+// branch never read: any defined value will do, and a constant would cost a move per iteration.
+// PK_UNREAD names a value that dies at that point, so the register allocator gives both one
+// register and no instruction is issued (a reminder at the use site, not an operation).
+#define PK_UNREAD(v) (v)
 
 // lane state (VGPRs for the whole launch).  Never select between two fields by reference: that
 // makes LLVM take field addresses and spill the struct to scratch.
@@ -146,8 +172,8 @@ struct St {
     u32 timac;            // TIMA_counter
     u32 mbc;              // rombank | rambank<<8 | ram_enabled<<16 | memorymodel<<24
     u32 misc;             // joypad directional | standard<<8 | (ly_window+1)<<16
-    u32 rb;               // LDS byte offset of the switchable ROM bank, PK_NO_BANK = not staged
-    u32 rlim;             // ROM addresses below it are staged: 0x8000, or 0x4000 when rb = PK_NO_BANK
+    u32 rb;               // LDS byte offset of the switchable ROM bank - 0x4000 (index = address + rb)
+    u32 rlim;             // ROM addresses below it are staged: 0x8000, or 0x4000 when the bank is not
     u32 lim;              // tick_lim(): clock below it = no LCD event, no LCD-off frame end, timer off,
                           // no frame watchdog
     u32 npend;            // latched, not yet rasterised lines
@@ -170,9 +196,13 @@ __device__ __forceinline__ void hcode_st(const Ctx& c, u32 a, u32 v) {
     const u32 row = sel(a - 0xFF80u < PK_HC_ROWS, a - 0xFF80u, PK_HC_ROWS);
     lds_rom[PK_HC_BASE + c.loc * PK_HC_STRIDE + row] = (u8)v;
 }
+// a plain-RAM write at a (and a +- 1 for 16-bit writes) that may touch the mirrored HRAM bytes:
+// only those writes update the mirror (a rare branch on the common path: code and the few HRAM
+// variables there are written seldom)
+__device__ __forceinline__ bool near_hcode(u32 a) { return a - 0xFF7Fu < PK_HC_ROWS + 2u; }
 
 // fast RAM: VRAM, WRAM, echo, OAM/unusable, HRAM — plain bytes of the image with no side effects
-__device__ __forceinline__ bool ram_region(u32 a) { return ((0xD0u >> (a >> 13)) & 1u) != 0u; }  // 0x8000, 0xC000, 0xE000
+__device__ __forceinline__ bool ram_region(u32 a) { return __builtin_amdgcn_ubfe(0xD0u, a >> 13, 1u) != 0u; }  // 0x8000, 0xC000, 0xE000
 // IO registers FF00-FF7F and IE (FFFF): a ^ 0x7F maps exactly those to the range FF00-FF80
 __device__ __forceinline__ bool io_addr(u32 a) { return ((a ^ 0x7Fu) - 0xFF00u) <= 0x80u; }
 __device__ __forceinline__ bool fast_ram(u32 a) { return ram_region(a) && !io_addr(a); }
@@ -183,7 +213,7 @@ __device__ __forceinline__ u32 fast_phys(u32 a) {
 __device__ __forceinline__ bool vram_or_oam(u32 a) { return (a >= 0x8000u && a < 0xA000u) || (a >= 0xFE00u && a < 0xFEA0u); }
 // ROM address staged in LDS?  and its LDS byte index
 __device__ __forceinline__ bool rom_staged(const St& s, u32 a) { return a < s.rlim; }
-__device__ __forceinline__ u32 rom_lds_index(const St& s, u32 a) { return sel(a < 0x4000u, a, s.rb + (a & 0x3FFFu)); }
+__device__ __forceinline__ u32 rom_lds_index(const St& s, u32 a) { return a + sel(a < 0x4000u, 0u, s.rb); }
 // byte index in the global ROM of a switchable-bank address (0x4000-0x7FFF)
 __device__ __forceinline__ u32 rom_global_index(const PkStepArgs& A, const St& s, u32 a) {
     return (((s.mbc & 0xFFu) & A.rom_bank_mask) << 14) | (a & 0x3FFFu);
@@ -203,12 +233,18 @@ __device__ __forceinline__ u32 rom_global_index(const PkStepArgs& A, const St& s
 #define PK_SLACK_MARGIN (2u * (FRAME_CYCLES / 4u) + 64u)
 __device__ __forceinline__ u32 tick_lim(const St& s, int slack) {
     const int e = (int)s.clock + slack - (int)PK_SLACK_MARGIN;
-    const u32 lim = sel(s.tim0 & (4u << 24), 0u, sel(s.lcd0 & 0x80u, s.target, FRAME_CYCLES));
+    // 0 also while the CPU is halted (the HALT instruction's microcode zeroes it: pk_exec)
+    const u32 lim = sel((s.tim0 & (4u << 24)) | (s.cpu & CPU_HALT), 0u, sel(s.lcd0 & 0x80u, s.target, FRAME_CYCLES));
     return min(lim, e > 0 ? (u32)e : 0u);
 }
 __device__ __forceinline__ u32 slot_base(u32 bank) {
     const int sl = lds_slot[bank & 127u];
     return sl >= 0 ? (u32)sl * 0x4000u : PK_NO_BANK;
+}
+// the switchable bank's LDS slot (slot_base), or PK_NO_BANK: rb and the staged-address limit
+__device__ __forceinline__ void set_rom_bank(St& s, u32 base) {
+    s.rb = base - 0x4000u;   // (unused when the bank is not staged: rom_lds_index is behind rom_staged)
+    s.rlim = sel(base != PK_NO_BANK, 0x8000u, 0x4000u);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -266,7 +302,7 @@ __device__ __forceinline__ void key_event(St& s, u32 button, bool pressed) {
     if (button < 4u) nd = pressed ? (nd & ~b) : (nd | b);
     else ns = pressed ? (ns & ~b) : (ns | b);
     s.misc = (s.misc & 0xFFFF0000u) | nd | (ns << 8);
-    if (((od ^ nd) & od) || ((os ^ ns) & os)) s.cpu |= 0x10u << 16;
+    if (((od ^ nd) & od) || ((os ^ ns) & os)) s.cpu = cpu_sync_pend(s.cpu | 0x10u << 16);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -327,8 +363,7 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
         } else if (a < 0x4000u) {
             v &= 0x7Fu;
             s.mbc = setb8(s.mbc, 0, v == 0u ? 1u : v);
-            s.rb = slot_base((s.mbc & 0xFFu) & A.rom_bank_mask);
-            s.rlim = sel(s.rb != PK_NO_BANK, 0x8000u, 0x4000u);
+            set_rom_bank(s, slot_base((s.mbc & 0xFFu) & A.rom_bank_mask));
         } else if (a < 0x6000u) {
             s.mbc = setb8(s.mbc, 8, v);
         }
@@ -351,7 +386,7 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
             case 0xFF05: s.tim0 = setb8(s.tim0, 8, v); break;
             case 0xFF06: s.tim0 = setb8(s.tim0, 16, v); break;
             case 0xFF07: s.tim0 = setb8(s.tim0, 24, v & 7u); break;
-            case 0xFF0F: s.cpu = setb8(s.cpu, 16, v); break;
+            case 0xFF0F: s.cpu = cpu_sync_pend(setb8(s.cpu, 16, v)); break;
             case 0xFF40:
                 lcd_unfold(s);
                 lcd_set_lcdc(s, v);
@@ -396,7 +431,7 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
             case 0xFF49: s.lcd2 = setb8(s.lcd2, 16, v); break;
             case 0xFF4A: s.lcd1 = setb8(s.lcd1, 16, v); break;
             case 0xFF4B: s.lcd1 = setb8(s.lcd1, 24, v); break;
-            case 0xFFFF: s.cpu = setb8(s.cpu, 8, v); break;
+            case 0xFFFF: s.cpu = cpu_sync_pend(setb8(s.cpu, 8, v)); break;
             default:
                 if (a >= 0xFF10u && a < 0xFF40u) break;  // sound: not emulated
                 st_img(c, PK_P_IO + (a & 0xFFu), v);
@@ -577,12 +612,13 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     const u32 w0 = s.w0, w1 = s.w1, sp = s.sp;
     const u32 F = (w1 >> 16) & 0xFFu;
     const u32 pcn = (pc + (D & 3u)) & 0xFFFFu;
-    const u32 taken = (((F | 0x100u) >> ((D >> PK_DB_CPOS) & 15u)) & 1u) ^ bit(D, PK_DB_CINV);
+    // the condition as a lane mask: bit CPOS of (F | 0x100) ^ CINV, sign-extended
+    const u32 tkm = (u32)__builtin_amdgcn_sbfe((int)(F | 0x100u), (D >> PK_DB_CPOS) & 15u, 1u) ^ bmask(D, PK_DB_CINV);
     u32 addr0 = 0, addr1 = 0, o0 = 0, o1 = 0;
     bool pair = false, fast01 = false;
+    // operand pools: registers (w1:w0) and ext (q1:q0) = instruction bytes, m0|m1 and SP
+    const u32 asrc = perm(w1, w0, m.AR) | perm(sp << 16, bytes, m.AE);
     {
-        // operand pools: registers (w1:w0) and ext (q1:q0) = instruction bytes, m0|m1 and SP
-        const u32 asrc = perm(w1, w0, m.AR) | perm(sp << 16, bytes, m.AE);
         addr0 = (asrc + (u32)sfield(D, PK_DB_AOFF, 2)) & 0xFFFFu;
         addr1 = (addr0 + (u32)sfield(D, PK_DB_ADIR, 2)) & 0xFFFFu;
         // image offsets of both addresses, shared by the fast read and write paths
@@ -602,13 +638,17 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     u32 m16 = 0;
     {
         const bool rram = rd & fast01;  // addr1 == addr0 for 1-byte reads
-        // staged ROM is 16 KB-aligned: inside one block addr1 is staged iff addr0 is, at index + ADIR
-        // ALL: every ROM bank is staged in LDS (a cartridge of <= the kernel's slots), so the switchable
-        // bank is staged whatever it is
-        const bool rrom = rd & (ALL ? addr0 < 0x8000u : rom_staged(s, addr0)) & pair;
-        // each source has its own result registers, merged by OR below: sharing one register
-        // would make the LDS ROM read wait for the image load of other lanes (write-after-write)
-        u32 rm0 = 0, rm1 = 0, om0 = 0, om1 = 0, xm = 0;
+        // one-byte reads of staged ROM (a two-byte read there — POP/RET with SP in ROM — takes the
+        // rare path); ALL: every ROM bank is staged in LDS (a cartridge of <= the kernel's slots), so
+        // the switchable bank is staged whatever it is
+        const bool rrom = (bit(D, PK_DB_RD1) != 0u) & (ALL ? addr0 < 0x8000u : rom_staged(s, addr0));
+        // The image loads and the LDS ROM read have registers of their own (sharing one would make
+        // the LDS read wait for the image loads of other lanes: write-after-write); the rare paths
+        // write the LDS read's register, after it.  A lane reads only the source it loaded: the
+        // initial values are never read, and are values that die here (PK_UNREAD), so the
+        // registers need no zeroing moves.  (m16 is unspecified for an instruction without a read:
+        // no selector takes it.)
+        u32 rm0 = PK_UNREAD(m.AR), rm1 = PK_UNREAD(m.AE), om = PK_UNREAD(asrc);
         if (rram) {
             // a one-byte read has o1 == o0 (ADIR 0): its second load hits the same line, and m1 is
             // not taken for it, so the load needs no test of its own
@@ -617,30 +657,37 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
             PK_MEMREF(c.env, 0u, fast_phys(addr0));
             if (rd2) PK_MEMREF(c.env, 0u, fast_phys(addr1));
         }
-        if (rrom) {
-            const u32 i0 = rom_lds_index(s, addr0);
-            om0 = lds_rom[i0];
-            om1 = lds_rom[i0 + (u32)sfield(D, PK_DB_ADIR, 2)];  // == om0 for 1-byte reads
-        }
-        if (PK_RARE(rd & !rram & !rrom)) {  // rare: IO registers (LY, STAT, joypad, ...), SRAM, unstaged ROM
+        if (rrom) om = lds_rom[rom_lds_index(s, addr0)];
+        if (PK_RARE(rd & !rram & !rrom)) {  // rare: IO registers (LY, STAT, joypad, ...), SRAM, unstaged ROM, DAA
             PK_STAMP_AT(0);
-            if (!rd2 & (addr0 >= 0xFF00u) & ((addr0 < 0xFF80u) | (addr0 == 0xFFFFu))) {
-                xm = io_read(c, s, addr0);
+            if (bit(D, PK_DB_DAA)) {
+                // DAA (opcodes.py DAA_27): its microcode reads two bytes at 0xFFFF (IE: never a fast
+                // or staged read) to land here, and takes the result as POP AF takes m1|m0: A = m1,
+                // F = m0 & 0xF0 — so the common path carries no DAA test of its own
+                const u32 a = w1 >> 24;
+                u32 corr = sel(F & 0x20u, 0x06u, 0u) | sel(F & 0x10u, 0x60u, 0u);
+                corr |= sel(F & 0x40u, 0u, sel((a & 0x0Fu) > 0x09u, 0x06u, 0u) | sel(a > 0x99u, 0x60u, 0u));
+                const u32 res = sel(F & 0x40u, a - corr, a + corr) & 0xFFu;
+                om = (F & 0x40u) | sel(res == 0u, 0x80u, 0u) | sel(corr & 0x60u, 0x10u, 0u) | (res << 8);
+            } else if (!rd2 & (addr0 >= 0xFF00u) & ((addr0 < 0xFF80u) | (addr0 == 0xFFFFu))) {
+                om = io_read(c, s, addr0);
                 PK_MEMREF(c.env, 2u, addr0);
                 ev |= PK_EV_RD_IO;
             } else if ((addr0 - 0x4000u < 0x4000u) & pair) {  // unstaged switchable bank: the global ROM
                 const u32 ga = rom_global_index(A, s, addr0);
-                xm = A.rom[ga] | sel(rd2, (u32)A.rom[ga + (u32)sfield(D, PK_DB_ADIR, 2)] << 8, 0u);
+                om = A.rom[ga] | sel(rd2, (u32)A.rom[ga + (u32)sfield(D, PK_DB_ADIR, 2)] << 8, 0u);
                 ev |= PK_EV_RD_ROMG;
             } else {
                 const St t = s;
-                xm = pk_read_slow(&A, c.g, c.lane, c.loc, &t, addr0, addr1, rd2 ? 1u : 0u);
+                om = pk_read_slow(&A, c.g, c.lane, c.loc, &t, addr0, addr1, rd2 ? 1u : 0u);
                 ev |= PK_EV_RD_ROMG;
             }
             PK_STAMP_AT(1);
         }
         // m0 | m1 << 8 (m1 is only meaningful for two-byte reads: one-byte operands select m0 alone)
-        m16 = rm0 | om0 | xm | ((rm1 | om1) << 8);
+        // (the byte pairs by v_perm: a shift would be pushed into the load branches, each then
+        // waiting there for its own loads)
+        m16 = sel(rram, perm(rm1, rm0, 0x0C0C0400u), om);
         ev |= sel(rd, PK_EV_RD | sel(rd2, PK_EV_RD2, 0u) | sel(rram, PK_EV_RD_RAM, 0u) | sel(rrom, PK_EV_RD_ROMLDS, 0u)
                       | sel(addr0 >= 0xFF80u && addr0 < 0xFFFFu, PK_EV_HRAM, 0u)
                       | sel(addr0 >= 0xC000u && addr0 < 0xFE00u, PK_EV_RD_WRAM, 0u), 0u);
@@ -649,14 +696,14 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     PK_STAMP_AT(0);
 
     // ---------------- fused datapath ----------------
-    const u32 q1 = m16 | (sp << 16);
+    const u32 q1 = perm(sp, m16, 0x05040100u);   // m0 | m1 << 8 | SP << 16
     const u32 X = perm(w1, w0, m.XR) | perm(q1, bytes, m.XE);
     const u32 Y = perm(w1, w0, m.YR) | perm(q1, bytes, m.YE) | m.YC;
-    const bool right = bit(U, PK_US_RIGHT) != 0u;
+    const u32 right = bmask(U, PK_US_RIGHT);
     u32 cin = 0, r = 0, cvx = 0, rs = 0, lres = 0;
     // carry-in of the adder, or the bit shifted in by the right-shift unit: bit CW of
     // (X | F << 16) ^ CI (F.C at bit 20, X's bits 7/0, bit 16 = 0 for the constants)
-    cin = ((((X & 0xFFFFu) | (w1 & 0xFFFF0000u)) ^ m.CI) & m.CW) != 0u ? 1u : 0u;
+    cin = min((((X & 0xFFFFu) | (w1 & 0xFFFF0000u)) ^ m.CI) & m.CW, 1u);
     // adder: r = X + Y ^ YX + cin (YX = 0x1FFFF subtracts); X ^ Y ^ r = the carry (borrow) into
     // each bit.  Left rotates and shifts are X + X + (0 / F.C / bit 7): bit 8 is the carry out
     r = X + (Y ^ m.YX) + cin;
@@ -664,31 +711,24 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     // right-shift unit: RRC RRA RR SRA SRL ((X | in << 8 | X.0 << 9) >> 1: bit 8 = the bit
     // shifted out) and SWAP ((X | X << 8) >> 4)
     {
-        const bool swap = bit(U, PK_US_SWAP) != 0u;
-        rs = (X | (sel(swap, X, cin | ((X & 1u) << 1)) << 8)) >> sel(swap, 4u, 1u);
+        const u32 swap = bmask(U, PK_US_SWAP);
+        rs = (X | (msel(swap, X, cin | ((X & 1u) << 1)) << 8)) >> msel(swap, 4u, 1u);
     }
     // logic: (X & Y) and/or (X ^ Y) (OR = both); loads are 0xFF AND Y
     lres = ((X & Y) & (u32)sfield(U, PK_US_LAND, 1)) | ((X ^ Y) & (u32)sfield(U, PK_US_LXOR, 1));
-    u32 res8 = sel(bit(U, PK_US_LOGIC), lres, sel(right, rs, r)) & 0xFFu;
+    const u32 res8 = msel(bmask(U, PK_US_LOGIC), lres, msel(right, rs, r)) & 0xFFu;
     // flags: F' = (F & FK) | ((Z | H | C | FC) & FM), H/C = carry bits 4/8 (12/16 for ADD HL) or
     // the right unit's shifted-out bit 8
     u32 nf = F;
     {
-        const u32 cs = sel(right, rs, cvx) >> (bit(U, PK_US_HSH8) * 8u);
+        const u32 cs = msel(right, rs, cvx) >> (bit(U, PK_US_HSH8) * 8u);
         const u32 fv = sel(res8 == 0u, 0x80u, 0u) | ((cs << 1) & 0x20u) | ((cs >> 4) & 0x10u) | K;
         nf = ((F & (K >> 8)) | (fv & (K >> 16))) & 0xFFu;
-        nf = sel(bit(U, PK_US_FPOP), m16 & 0xF0u, nf);
-    }
-    if (PK_RARE(bit(D, PK_DB_DAA))) {  // DAA (opcodes.py DAA_27), rare
-        const u32 a = w1 >> 24;
-        u32 corr = sel(F & 0x20u, 0x06u, 0u) | sel(F & 0x10u, 0x60u, 0u);
-        corr |= sel(F & 0x40u, 0u, sel((a & 0x0Fu) > 0x09u, 0x06u, 0u) | sel(a > 0x99u, 0x60u, 0u));
-        res8 = sel(F & 0x40u, a - corr, a + corr) & 0xFFu;
-        nf = (F & 0x40u) | sel(res8 == 0u, 0x80u, 0u) | sel(corr & 0x60u, 0x10u, 0u);
+        nf = msel(bmask(U, PK_US_FPOP), m16 & 0xF0u, nf);
     }
     // register writeback: val = res16 | F' << 16 | res8 << 24 through the per-op byte selectors
     // (res16: the adder, or HL +- 1 for (HL+)/(HL-); bytes 2-3 of either are not taken)
-    const u32 u16 = sel(bit(U, PK_US_R16HL), w1 + (u32)sfield(U, PK_US_HLINC, 2), r);
+    const u32 u16 = msel(bmask(U, PK_US_R16HL), w1 + (u32)sfield(U, PK_US_HLINC, 2), r);
     {
         const u32 val = perm(nf | (res8 << 8), u16, 0x05040100u);
         s.w0 = perm(val, w0, m.S0);
@@ -700,24 +740,26 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     s.pc = pcn;
     {
         const u32 tgt = (X + Y + (pcn & m.V)) & 0xFFFFu;
-        const bool jump = bit(U, PK_US_JUMP) != 0u && taken != 0u;
-        s.pc = sel(jump, tgt, pcn);
-        ev |= sel(jump, PK_EV_JUMP, 0u);
+        const u32 jump = bmask(U, PK_US_JUMP) & tkm;
+        s.pc = msel(jump, tgt, pcn);
+        ev |= sel(jump != 0u, PK_EV_JUMP, 0u);
     }
-    x.cycles = ((D >> PK_DB_CYC) & 7u) * 4u + sel(taken != 0u, ((D >> PK_DB_XCYC) & 3u) * 4u, 0u);
+    x.cycles = ((m.V >> 16) & 0xFFu) + ((m.V >> 24) & tkm);   // (pk_ucode.h: V word)
     {
-        const u32 sp2 = (sp + ((u32)sfield(U, PK_US_SPD, 3) & (0u - taken))) & 0xFFFFu;
-        s.sp = sel(bit(U, PK_US_SPW), u16 & 0xFFFFu, sp2);
+        const u32 sp2 = (sp + ((u32)sfield(U, PK_US_SPD, 3) & tkm)) & 0xFFFFu;
+        s.sp = msel(bmask(U, PK_US_SPW), u16 & 0xFFFFu, sp2);
     }
     // IME / HALT / CRASH / QUEUED: (cpu & keep) | set from the microcode
     s.cpu = (s.cpu & (0xFFFFFFF0u | ((K >> 24) & 15u))) | (K >> 28);
+    s.lim = msel(bmask(K, 28 + 1), 0u, s.lim);   // HALT (or CRASH) set: the tick stage runs (tick_lim)
+    PK_OPAQUE(s.cpu);   // (else LLVM keeps the incoming word live too: a loop-end copy)
 
     // the write: wv0 at addr0, wv1 at addr1 (16-bit writes: low byte first in memory; pushes
     // SP-2, SP-1); the stage itself (pk_write) runs after the secondary op
-    x.wr = bit(D, PK_DB_WR) != 0u && taken != 0u;
+    x.wr = (D & tkm & (1u << PK_DB_WR)) != 0u;
     x.wr2 = bit(D, PK_DB_WR2) != 0u;
     x.wram = x.wr & fast01;
-    const u32 wv = sel(bit(U, PK_US_W16), sel(bit(U, PK_US_WPC), pcn, X), res8);
+    const u32 wv = msel(bmask(U, PK_US_W16), msel(bmask(U, PK_US_WPC), pcn, X), res8);
     x.wv0 = wv & 0xFFu;
     x.wv1 = (wv >> 8) & 0xFFu;
     x.addr0 = addr0;
@@ -750,8 +792,10 @@ __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc&
         c.g[sel(w2, x.o1, dummy)] = (u8)x.wv1;
         if (x.wram) PK_MEMREF(env, 1u, fast_phys(x.addr0));
         if (w2) PK_MEMREF(env, 1u, fast_phys(x.addr1));
-        hcode_st(c, sel(x.wram, x.addr0, 0u), x.wv0);   // address 0: the mirror's dummy row
-        hcode_st(c, sel(w2, x.addr1, 0u), x.wv1);
+        if (PK_RARE(x.wram & near_hcode(x.addr0))) {
+            hcode_st(c, x.addr0, x.wv0);
+            hcode_st(c, sel(x.wr2, x.addr1, 0u), x.wv1);   // address 0: the mirror's dummy row
+        }
     } else if (x.wram) {
         // VRAM / OAM change while rendered lines are pending: rasterise them first (rare)
         // (lines are pending only in the rendered frame: test that first, alone)
@@ -767,11 +811,13 @@ __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc&
         }
         c.g[x.o0] = (u8)x.wv0;
         PK_MEMREF(env, 1u, fast_phys(x.addr0));
-        hcode_st(c, x.addr0, x.wv0);
         if (x.wr2) {
             c.g[x.o1] = (u8)x.wv1;
             PK_MEMREF(env, 1u, fast_phys(x.addr1));
-            hcode_st(c, x.addr1, x.wv1);
+        }
+        if (PK_RARE(near_hcode(x.addr0))) {
+            hcode_st(c, x.addr0, x.wv0);
+            hcode_st(c, sel(x.wr2, x.addr1, 0u), x.wv1);   // address 0: the mirror's dummy row
         }
     }
     PK_STAMP_AT(2);
@@ -856,7 +902,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
     s.w1 = perm(R[PK_R_W1 * np + env], R[PK_R_W1 * np + env], 0x02030100u);  // L H A F -> L H F A
     s.sp = R[PK_R_SP * np + env];
     s.pc = R[PK_R_PC * np + env];
-    s.cpu = R[PK_R_CPU * np + env];
+    s.cpu = cpu_sync_pend(R[PK_R_CPU * np + env]);
     s.clock = R[PK_R_CLOCK * np + env];
     s.target = R[PK_R_TARGET * np + env];
     s.lcd0 = R[PK_R_LCD0 * np + env];
@@ -870,8 +916,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
     }
     s.mbc = R[PK_R_MBC * np + env];
     s.misc = R[PK_R_MISC * np + env];
-    s.rb = slot_base((s.mbc & 0xFFu) & A.rom_bank_mask);
-    s.rlim = sel(s.rb != PK_NO_BANK, 0x8000u, 0x4000u);
+    set_rom_bank(s, slot_base((s.mbc & 0xFFu) & A.rom_bank_mask));
     s.npend = 0;
     s.blank = 0;
     s.frame_done = 0;
@@ -897,8 +942,10 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
     s.lim = tick_lim(s, slack);
     // software pipeline: the next instruction's bytes and microcode entry, loaded from LDS at the
     // end of the previous iteration (after its writes, so bank switches and HRAM code stores are
-    // seen) while the timer/LCD work runs; pf = 0 -> fetch and decode at the top instead
-    u32 pf = 0, pbytes = 0;
+    // seen) while the timer/LCD work runs.  pbytes = PK_COPY_W0 means "not prefetched": fetch and
+    // decode at the top instead (the block-copy loop's own first bytes, which take the rare loop-top
+    // stage anyway, are fetched there again), so the loop top tests one value for both
+    u32 pbytes = PK_COPY_W0;
     uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0, p2 = p0, p3 = p0;
 #ifdef PK_STAMP
     uint64_t st_acc[PK_NSTAMP] = {}, st_prev = __builtin_amdgcn_s_memtime(), st_iter = 0;
@@ -915,18 +962,19 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         // ---------------- front-end: cpu.tick / check_interrupts ----------------
         // common case (running, nothing pending): execute at pc; otherwise the full PyBoy order
         const u32 cpu0 = s.cpu;
-        const u32 pend = (cpu0 >> 8) & (cpu0 >> 16) & 0x1Fu;
         bool exec = true, doint = false, dispatch = false;
         u32 pc = s.pc, intflag = 0;
         u32 bytes = pbytes;
         uint4 e0 = p0, e1 = p1, e2 = p2, e3 = p3;
         // the three rare stages of the loop top (interrupts / HALT, a fetch that was not prefetched,
         // a block-copy or LY-poll loop at pc) sit behind one test: the common path pays one branch
-        const bool fe_rare = ((cpu0 & (CPU_CRASH | CPU_HALT | CPU_QUEUED)) | pend) != 0u;
+        const bool fe_rare = (cpu0 & (CPU_CRASH | CPU_HALT | CPU_QUEUED | CPU_PEND)) != 0u;
         const bool loop_at = (pbytes == PK_COPY_W0) | ((pbytes & 0x00FFFFFFu) == PK_POLL_W0);
-        if (PK_RARE(fe_rare | !pf | loop_at)) {
+        bool pf = true;   // prefetched (iteration statistics only)
+        if (PK_RARE(fe_rare | loop_at)) {
+        pf = !fe_rare & (pbytes != PK_COPY_W0);
         if (fe_rare) {
-            pf = 0;
+            const u32 pend = (cpu0 >> 8) & (cpu0 >> 16) & 0x1Fu;
             const bool crashed = (cpu0 & CPU_CRASH) != 0u;
             const bool halted = (cpu0 & CPU_HALT) != 0u;
             const bool queued = (cpu0 & CPU_QUEUED) != 0u;
@@ -936,10 +984,11 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
             exec = !crashed && !doint && (!halted || queued);
             pc = (pc + sel((doint && halted) || wake, 1u, 0u)) & 0xFFFFu;
             intflag = pend & (0u - pend);
-            s.cpu = sel(doint, (cpu0 | CPU_QUEUED) & ~CPU_HALT, sel(wake, cpu0 & ~CPU_HALT, cpu0)) ^ sel(dispatch, intflag << 16, 0u);
+            s.cpu = cpu_sync_pend(sel(doint, (cpu0 | CPU_QUEUED) & ~CPU_HALT, sel(wake, cpu0 & ~CPU_HALT, cpu0))
+                                  ^ sel(dispatch, intflag << 16, 0u));
         }
 
-        // ---------------- fetch + microcode entry (prefetched, or here when pf = 0) ----------------
+        // ---------------- fetch + microcode entry (prefetched, or here when pf = false) ----------------
         if (!pf) {
             PK_STAMP_AT(8);
             const bool flds = rom_staged(s, pc) && (pc & 0x3FFFu) < 0x3FFEu;
@@ -997,7 +1046,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         icount -= sel(exec, 0u, 1u);   // an interrupt dispatch or idle iteration emulates no instruction
         }
         icount += 1u;   // (the rare loop-top stage takes it back for an interrupt dispatch / idle iteration)
-        ev |= sel(exec, PK_EV_EXEC | sel((bytes & 0xFFu) == 0xCBu, PK_EV_CB, 0u), 0u) | sel(pf != 0u, PK_EV_F_LDS, 0u)
+        ev |= sel(exec, PK_EV_EXEC | sel((bytes & 0xFFu) == 0xCBu, PK_EV_CB, 0u), 0u) | sel(pf, PK_EV_F_LDS, 0u)
             | sel(dispatch, PK_EV_INT, 0u) | sel(!exec && !dispatch, PK_EV_IDLE, 0u);
         if (exec && !((bytes == PK_COPY_W0) | ((bytes & 0x00FFFFFFu) == PK_POLL_W0)))
             PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, bytes & 0xFFu);
@@ -1024,15 +1073,16 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         // (ROM code has 4), and none of them an IO register (DIV and a folded STAT change with the clock).
         {
             const u32 len2 = u2.y & 3u;
-            // both instructions within the fetched bytes: 4 for ROM code (and inside its 16 KiB bank:
-            // the LDS slots of other banks follow it), 3 for code in RAM
-            const u32 n2 = (D & 3u) + len2;
+            // a secondary op (len2 != 0) and both instructions within the fetched bytes,
+            // (D & 3) + len2 <= avail: 4 for ROM code (and inside its 16 KiB bank: the LDS slots of
+            // other banks follow it), 3 for code in RAM.  As one compare: len2 - 1 wraps for len2 = 0,
+            // and avail - (D & 3) saturates (v_sub clamp) for an instruction at the bank end
             const u32 avail = sel(pc < 0x8000u, min(4u, 0x4000u - (pc & 0x3FFFu)), 3u);
-            const bool lenok = n2 <= avail;
+            const bool lenok = len2 - 1u < (avail > (D & 3u) ? avail - (D & 3u) : 0u);
             const bool ramok = (pc < 0x8000u) | (!wr & !(pc - 0xFEFEu < 0x82u));
             // next LCD event / LCD-off frame end, 0 with the timer on (tick_lim)
             // (s.lim also bounds the watchdog: clock + cycles < lim implies cycles < slack)
-            const bool fuse = (len2 != 0u) & (s.clock + cycles < s.lim) & !(wr & !wram) & ramok & lenok;
+            const bool fuse = (s.clock + cycles < s.lim) & !(wr & !wram) & ramok & lenok;
             const u32 M2 = sel(fuse, u2.y, PK_U2_NONE_Y);
             // X (pair, or register in byte 0); Y = register | immediate n, ^ the subtract mask, + delta;
             // one adder X + Y + carry-in (ADC/SBC: F.C; SUB/SBC/CP: ^ 1), a logic unit (AND XOR OR),
@@ -1085,7 +1135,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         // next instruction in an unstaged switchable bank (most of a 64-bank cartridge): its two
         // global-ROM dwords are requested now, so their latency overlaps the write stage (a lane
         // whose write switches the ROM bank refetches at the top of the next iteration)
-        u32 ng0 = 0, ng1 = 0, nga = 0;
+        u32 ng0 = PK_UNREAD(u2b.x), ng1 = PK_UNREAD(u2b.y), nga = PK_UNREAD(u2b.z);   // read only where loaded (fg)
         const bool nfg = !ALL & !rom_staged(s, s.pc) & (s.pc - 0x4000u < 0x3FFEu)
                        & !(s.pc - 0xFF80u < 0x7Du);
         if (nfg) {
@@ -1123,7 +1173,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
             p1 = ucv[di * 4u + 1u];
             p2 = ucv[di * 4u + 2u];
             p3 = ucv[di * 4u + 3u];
-            pf = sel(fl | fh | fg, 1u, 0u);
+            pbytes = sel(fl | fh | fg, pbytes, PK_COPY_W0);
         }
 
 
@@ -1135,11 +1185,15 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         // works on the advanced clock, DIV and budget; its HALT block undoes and redoes them around
         // its own cycle count), so the common case is no separate branch with its own copies of them.
         const u32 clk2 = s.clock + cycles;
-        // timer on: lim 0; the watchdog (cycles + 1 > slack) is within clk2 >= lim (tick_lim)
-        const bool rare = (s.cpu & CPU_HALT) | (clk2 >= s.lim);
+        // timer on or CPU halted: lim 0; the watchdog (cycles + 1 > slack) is within clk2 >= lim (tick_lim)
+        const bool rare = clk2 >= s.lim;
         s.divacc += cycles;
         s.clock = clk2;
         slack -= (int)(cycles + 1u);
+        // opaque from here: otherwise LLVM folds the HALT block's undo (clock - cycles) back to the
+        // iteration's incoming clock and DIV, which keeps those registers live past the update and
+        // costs loop-end register copies on the common path
+        PK_PIN3(s.clock, s.divacc, s.cpu);
         if (PK_RARE(rare)) {
             const u32 tac = s.tim0 >> 24;
             // HALT skip-ahead: a halted CPU that nothing can wake before VBlank (no pending or queued
@@ -1273,7 +1327,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
                 s.clock %= FRAME_CYCLES;
                 s.blank |= s.render;
             }
-            s.cpu |= irq << 16;
+            s.cpu = cpu_sync_pend(s.cpu | irq << 16);
             PK_STAMP_AT(7);
             ev |= sel(s.frame_done != 0u || slack < 0, PK_EV_FRAME, 0u);
             if (PK_RARE((s.frame_done != 0u) | (slack < 0))) {  // frame end or watchdog
@@ -1322,7 +1376,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
     R[PK_R_W1 * np + env] = perm(s.w1, s.w1, 0x02030100u);
     R[PK_R_SP * np + env] = s.sp;
     R[PK_R_PC * np + env] = s.pc;
-    R[PK_R_CPU * np + env] = s.cpu;
+    R[PK_R_CPU * np + env] = s.cpu & ~CPU_PEND;
     R[PK_R_CLOCK * np + env] = s.clock;
     R[PK_R_TARGET * np + env] = s.target;
     R[PK_R_LCD0 * np + env] = s.lcd0;

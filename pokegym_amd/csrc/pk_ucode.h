@@ -23,7 +23,8 @@ enum { PK_UE_D = 0, PK_UE_U, PK_UE_K, PK_UE_V, PK_UE_XR, PK_UE_XE, PK_UE_YR, PK_
        PK_UE_S0, PK_UE_S1, PK_UE_YC, PK_UE_YX, PK_UE_CW, PK_UE_CI, PK_UE_WORDS };
 // stored words (what the kernel reads; the builder below works in the PK_UB_/PK_KB_ form):
 //   U  datapath control bits PK_US_*          K  FC | FK << 8 | FM << 16 | CPUAND << 24 | CPUOR << 28
-//   V  0xFFFF for JR (target = pc + len + Y), else 0
+//   V  0xFFFF for JR (target = pc + len + Y), else 0; | cycles << 16 | extra cycles when the
+//      condition holds << 24 (the D fields CYC/XCYC times 4: one add and one select in the kernel)
 //   YC Y constant (INC/DEC, CPL, BIT/RES/SET masks, RST vector)   YX 0x1FFFF when the adder subtracts
 //   CW/CI carry-in (adder) / shifted-in bit (right-shift unit) = bit CW of (X | F << 16) ^ CI:
 //         bit 20 = F.C, bit 7/bit 0 = X's top/bottom bit, bit 16 = constant 0 (with CI: constant 1)
@@ -60,6 +61,7 @@ enum { PK_UE_D = 0, PK_UE_U, PK_UE_K, PK_UE_V, PK_UE_XR, PK_UE_XE, PK_UE_YR, PK_
 #define PK_DB_WR 4        // write wv0 at addr0
 #define PK_DB_WR2 5       // write wv1 at addr1
 #define PK_DB_ASP 6       // (builder only) address source SP        -> AE selector
+#define PK_DB_RD1 6       // (stored word) a one-byte read (RD, not RD2): the LDS-staged ROM path
 #define PK_DB_NOFUSE 8    // (stored word) no secondary op may follow in the same iteration (pk_u2_entry)
 #define PK_DB_AIMM 7      // (builder only) address source immediate -> AE selector
 #define PK_DB_AHN 8       // (builder only) immediate address 0xFF00|n
@@ -73,7 +75,7 @@ enum { PK_UE_D = 0, PK_UE_U, PK_UE_K, PK_UE_V, PK_UE_XR, PK_UE_XE, PK_UE_YR, PK_
 #define PK_DB_IME 26      // 2 bits: 0 keep 1 clear 2 set
 #define PK_DB_HALT 28     // set HALT
 #define PK_DB_CRASH 29    // set CRASH|HALT (illegal opcode)
-#define PK_DB_DAA 30      // DAA (rare path)
+#define PK_DB_DAA 30      // DAA (the rare read block: its microcode reads 0xFFFF twice)
 #define PK_DB_YSP 31      // (builder only) Y = SP
 enum { PK_T_NONE = 0, PK_T_IMM, PK_T_HL, PK_T_JR, PK_T_M16, PK_T_RST };
 enum { PK_J_NONE = 0, PK_J_XY = 1, PK_J_JR = 2 };  // stored: target = X | Y (operands chosen below) or pc+2+e
@@ -236,7 +238,11 @@ static inline PkUop pk_uop(int op) {
         case 0x76: o = pk_uop_base(0, 4); o.d |= pk_fld(1, PK_DB_HALT); return o;  // HALT: PC stays
         case 0xF3: o.d |= pk_fld(1, PK_DB_IME); return o;
         case 0xFB: o.d |= pk_fld(2, PK_DB_IME); return o;
-        case 0x27: o.d |= pk_fld(1, PK_DB_DAA); o.px = pk_sel8(7); pk_wb_r8(o, 7); return o;  // DAA (rare path)
+        case 0x27:  // DAA: computed in the kernel's rare read block, delivered as m1|m0 (A, F) like POP AF
+            o.d |= pk_fld(1, PK_DB_DAA) | pk_fld(1, PK_DB_RD) | pk_fld(1, PK_DB_RD2) | pk_sfld(-1, PK_DB_AOFF, 2);
+            o.u |= pk_fld(1, PK_UB_YMEM) | pk_fld(1, PK_UB_FPOP);
+            o.s1 = (o.s1 & 0x00FFFFFFu) | 0x05000000u;
+            return o;
         case 0x2F:  // CPL = A ^ 0xFF
             o.px = pk_sel8(7); o.k |= pk_fld(0xFF, PK_KB_YCONST);
             o.u |= pk_fld(2, PK_UB_R8) | pk_fld(1, PK_UB_LOP);
@@ -557,6 +563,7 @@ static inline void pk_store_uop(uint32_t* e, PkUop o, bool real) {
     if (o.d & pk_fld(1, PK_DB_ASP)) ae = PK_E_SP;
     else if (o.d & pk_fld(1, PK_DB_AIMM)) ae = (o.d & pk_fld(1, PK_DB_AHN)) ? PK_E_HN : PK_E_NN;
     e[PK_UE_D] = o.d & ~(pk_fld(1, PK_DB_ASP) | pk_fld(1, PK_DB_AIMM) | pk_fld(1, PK_DB_AHN) | pk_fld(1, PK_DB_YSP));
+    if ((o.d & pk_fld(1, PK_DB_RD)) && !rd2) e[PK_UE_D] |= pk_fld(1, PK_DB_RD1);
     // a secondary op may be fused after this one: executed instructions without control transfer,
     // IME/HALT/STOP changes or the rare DAA path (pk_u2_entry states the remaining conditions)
     if (!(real && ts == PK_T_NONE && !(o.d & (pk_fld(3, PK_DB_IME) | pk_fld(1, PK_DB_HALT) | pk_fld(1, PK_DB_CRASH) |
@@ -564,7 +571,7 @@ static inline void pk_store_uop(uint32_t* e, PkUop o, bool real) {
         e[PK_UE_D] |= pk_fld(1, PK_DB_NOFUSE);
     e[PK_UE_U] = us;
     e[PK_UE_K] = fconst | (fkeep << 8) | (fm << 16) | (cpu_keep << 24) | (cpu_set << 28);
-    e[PK_UE_V] = jrm;
+    e[PK_UE_V] = jrm | ((((o.d >> PK_DB_CYC) & 7u) * 4u) << 16) | ((((o.d >> PK_DB_XCYC) & 3u) * 4u) << 24);
     e[PK_UE_XR] = xe != PK_PZERO ? PK_PZERO : o.px;
     e[PK_UE_XE] = xe;
     e[PK_UE_YR] = ye != PK_PZERO ? PK_PZERO : o.py;

@@ -218,13 +218,15 @@ def boundary_rom() -> bytes:
     return build_rom("\n".join(L), n_banks=2, title="SEAMS")
 
 
-def hram_code_rom() -> bytes:
+def hram_code_rom(n_banks: int = 2) -> bytes:
     """Code run from all over HRAM: K1 fetches HRAM code from an LDS mirror of 0xFF80-0xFF9F only
     (where games keep the OAM-DMA routine) and from the RAM image elsewhere.  Routines sit inside
     the mirror (0xFF90), across its end (0xFF98-0xFF9F: the RET is fetched from the image),
     outside it (0xFFB0, 0xFFC0) and at the top of HRAM (0xFFF6: the RET's fetch reaches IE at
-    0xFFFF); two of them are rewritten every pass with joypad-dependent immediates (self-modifying
-    HRAM code: the mirror must follow the writes)."""
+    0xFFFF); two of them are rewritten every pass with joypad-dependent immediates, and the
+    mirrored loop's jr offset by a push (self-modifying HRAM code: the mirror must follow 8- and
+    16-bit writes).  n_banks = 64: the same code on a cartridge K1 cannot stage whole (the
+    unstaged-bank instance and its branch-free write stage)."""
     loop = "$04, $78, $81, $4f, $15, $20, $f9, $c9"        # inc b; ld a,b; add a,c; ld c,a; dec d; jr nz,-7; ret
     imm = "$3e, $00, $80, $47, $c9"                          # ld a,N; add a,b; ld b,a; ret
     L = ["section 0", "org $0040", "reti", "org $0048", "reti", "org $0050", "reti", "org $0058", "reti",
@@ -239,13 +241,16 @@ def hram_code_rom() -> bytes:
           "main:",
           "ld a, $10", "ldh [$00], a", "ldh a, [$00]", "ldh a, [$00]", "add a, c", "ld e, a",
           "ldh [$91], a",                        # rewrite the mirrored routine's immediate
+          "and $01", "add a, $f9", "ld h, a", "ld l, $20",   # and the loop's jr nz + offset (-7 / -6)
+          "ld sp, $ff9f", "push hl", "ld sp, $dff0",          # by a push (the offset is its 2nd byte)
+          "ld a, e",
           "xor $5a", "ldh [$c1], a",             # and the unmirrored one's
           "call $ff90", "ld d, 3", "call $ff98", "call $ffc0", "ld d, 2", "call $ffb0",
           "ld a, e", "and $03", "inc a", "ld d, a", "call $fff6",
           "ld a, b", "ld [$c000], a", "ld a, c", "ld [$c001], a",
           "jp main",
           "r_loop:", f"db {loop}", "r_imm:", f"db {imm}"]
-    return build_rom("\n".join(L), n_banks=2, title="HRAMCODE")
+    return build_rom("\n".join(L), n_banks=n_banks, title="HRAMCODE")
 
 
 def copydata_rom() -> bytes:

@@ -29,6 +29,7 @@
 #define __builtin_amdgcn_s_waitcnt(x) ((void)0)
 #define __builtin_nontemporal_store(v, p) (*(p) = (v))
 #define PK_PIN3(a, b, c) ((void)0)
+#define PK_OPAQUE(x) ((void)0)
 // lanes run one at a time: a ballot of this lane alone (uses test ballot(x) != 0 for "any lane")
 #define __builtin_amdgcn_ballot_w64(x) ((uint64_t)(bool)(x))
 // v_perm_b32: byte i of the result = byte sel.byte[i] of {hi, lo} (0-3 lo, 4-7 hi), 8-11 the sign
@@ -50,6 +51,22 @@ static inline uint32_t __builtin_amdgcn_perm(uint32_t hi, uint32_t lo, uint32_t 
     return r;
 }
 // v_alignbyte_b32: ({hi, lo} >> (8 * (sh & 3)))[31:0]
+// v_bfe_u32: width bits at offset (both & 31); width 0 -> 0
+static inline uint32_t __builtin_amdgcn_ubfe(uint32_t src, uint32_t off, uint32_t width) {
+    off &= 31u;
+    width &= 31u;
+    if (width == 0u) return 0u;
+    if (off + width >= 32u) return src >> off;
+    return (src << (32u - off - width)) >> (32u - width);
+}
+// v_bfe_i32: width bits at offset (both & 31), sign-extended; width 0 -> 0
+static inline int __builtin_amdgcn_sbfe(int src, uint32_t off, uint32_t width) {
+    off &= 31u;
+    width &= 31u;
+    if (width == 0u) return 0;
+    if (off + width >= 32u) return (int)src >> off;
+    return (int)((uint32_t)src << (32u - off - width)) >> (32u - width);
+}
 static inline uint32_t __builtin_amdgcn_alignbyte(uint32_t hi, uint32_t lo, uint32_t sh) {
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (sh & 3)));
 }

@@ -200,6 +200,16 @@ def test_hram_code_parity(shape, monkeypatch):
     assert not bad, bad[:4]
 
 
+def test_hram_code_parity_64_banks():
+    """The same code on a 64-bank cartridge: K1's unstaged-bank instance, whose write stage updates
+    the HRAM mirror behind its own rare branch (8- and 16-bit self-modifying writes)."""
+    from pokegym_amd.testrom.fuzz import hram_code_rom
+    n = 256
+    gpu, ref = _run_both(hram_code_rom(64), None, n, 4, 31)
+    bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
+    assert not bad, bad[:4]
+
+
 def warp_actions(n, seed=5):
     """Actions (6, n) from the warp fixture's state: columns 0..n/2-1 the recorded actions (they
     walk through a door at step 2: pkbench's map load with the LCD off for ~5 frames), the rest

@@ -46,10 +46,12 @@ def test_hostsim_game_64_banks():
     assert check(game_rom(64), 8, 8, 5) == []
 
 
-def test_hostsim_hram_code():
-    """Code fetched from inside, across and outside the LDS-mirrored HRAM bytes, self-modified."""
+@pytest.mark.parametrize("n_banks", [2, 64])
+def test_hostsim_hram_code(n_banks):
+    """Code fetched from inside, across and outside the LDS-mirrored HRAM bytes, self-modified by
+    8- and 16-bit writes; 64 banks: the unstaged-bank instance (branch-free write stage)."""
     from pokegym_amd.testrom.fuzz import hram_code_rom
-    assert check(hram_code_rom(), 8, 3, 5) == []
+    assert check(hram_code_rom(n_banks), 8, 3, 5) == []
 
 
 def test_hostsim_frame_watchdog():
