@@ -721,7 +721,7 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     // the right unit's shifted-out bit 8
     u32 nf = F;
     {
-        const u32 cs = msel(right, rs, cvx) >> (bit(U, PK_US_HSH8) * 8u);
+        const u32 cs = msel(right, rs, cvx) >> (U & (1u << PK_US_HSH8));   // >> 8 for ADD HL
         const u32 fv = sel(res8 == 0u, 0x80u, 0u) | ((cs << 1) & 0x20u) | ((cs >> 4) & 0x10u) | K;
         nf = ((F & (K >> 8)) | (fv & (K >> 16))) & 0xFFu;
         nf = msel(bmask(U, PK_US_FPOP), m16 & 0xF0u, nf);
@@ -1124,7 +1124,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
             // registers live there and costs register copies at the loop end
             PK_PIN3(s.w0, s.w1, s.sp);
             const u32 one = bit(M2, PK_U2B_ONE);
-            cycles += ((M2 >> PK_U2B_CYC) & 15u) * 4u + sel(tk2, 4u, 0u);
+            cycles += ((M2 >> PK_U2B_CYC) & 15u) + sel(tk2, 4u, 0u);
             slack -= (int)one;
             icount += one;
         }

@@ -28,10 +28,10 @@ enum { PK_UE_D = 0, PK_UE_U, PK_UE_K, PK_UE_V, PK_UE_XR, PK_UE_XE, PK_UE_YR, PK_
 //   YC Y constant (INC/DEC, CPL, BIT/RES/SET masks, RST vector)   YX 0x1FFFF when the adder subtracts
 //   CW/CI carry-in (adder) / shifted-in bit (right-shift unit) = bit CW of (X | F << 16) ^ CI:
 //         bit 20 = F.C, bit 7/bit 0 = X's top/bottom bit, bit 16 = constant 0 (with CI: constant 1)
-#define PK_US_HSH8 0      // H/C from carry bits 12/16 (ADD HL,rr), else 4/8
+#define PK_US_LOGIC 0     // result8 from the logic unit (loads: X = 0xFF AND Y), else adder / right unit
 #define PK_US_RIGHT 1     // result8 and C from the right-shift unit
 #define PK_US_SWAP 2      // right-shift unit: nibble swap
-#define PK_US_LOGIC 3     // result8 from the logic unit (loads: X = 0xFF AND Y), else adder / right unit
+#define PK_US_HSH8 3      // H/C from carry bits 12/16 (ADD HL,rr), else 4/8 (at bit 3: U & 8 is the shift)
 #define PK_US_JUMP 4      // control transfer to X + Y (+ pc + len for JR) when the condition holds
 #define PK_US_WPC 5       // 16-bit write value = return PC (else X)
 #define PK_US_W16 6       // write value 16-bit (else result8)
@@ -603,7 +603,7 @@ static inline void pk_store_uop(uint32_t* e, PkUop o, bool real) {
 // flags Z from res, H/C from the adder's carry vector (^ flip, & mask), constants ORed in.
 #define PK_U2B_LEN 0      // 2 bits length (0: no secondary op)
 #define PK_U2B_ONE 2      // 1: counts as an executed instruction
-#define PK_U2B_CYC 4      // 4 bits cycles/4 (JR: not taken)
+#define PK_U2B_CYC 4      // 4 bits cycles (JR: not taken; at most 8)
 #define PK_U2B_DELTA 8    // 8 bits signed: added to Y (INC/DEC)
 #define PK_U2B_CV 16      // 8 bits: JR taken when (F & mask) == cv, the mask in byte 2 of the x word;
                           //         1 for every other entry (F's low nibble is 0: never)
@@ -680,7 +680,7 @@ static inline void pk_u2_entry(uint32_t* e, int op) {
         }
     }
     e[0] = sel;
-    e[1] = (len << PK_U2B_LEN) | ((len ? 1u : 0u) << PK_U2B_ONE) | ((cyc / 4u) << PK_U2B_CYC)
+    e[1] = (len << PK_U2B_LEN) | ((len ? 1u : 0u) << PK_U2B_ONE) | (cyc << PK_U2B_CYC)
          | (((uint32_t)delta & 0xFFu) << PK_U2B_DELTA) | (cv << PK_U2B_CV) | (fm << PK_U2B_FM);
     e[2] = o.s0;
     e[3] = o.s1;
