@@ -602,7 +602,7 @@ struct Mc {   // a microcode entry (pk_ucode.h), one VGPR per word
 };
 struct Ex {   // what the rest of the iteration needs from the instruction
     u32 addr0, addr1, o0, o1, wv0, wv1, cycles;
-    bool wr, wr2, wram;
+    bool wr, wr2, wram, slow;   // slow: a write the generic bus path takes (wr & !wram)
 };
 template <bool PRIO, bool ALL>
 __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, const Mc& m, u32& ev, Ex& x PK_STAMP_PARAMS) {
@@ -759,6 +759,7 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     x.wr = (D & tkm & (1u << PK_DB_WR)) != 0u;
     x.wr2 = bit(D, PK_DB_WR2) != 0u;
     x.wram = x.wr & fast01;
+    x.slow = x.wr & !fast01;
     const u32 wv = msel(bmask(U, PK_US_W16), msel(bmask(U, PK_US_WPC), pcn, X), res8);
     x.wv0 = wv & 0xFFu;
     x.wv1 = (wv >> 8) & 0xFFu;
@@ -788,8 +789,11 @@ __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc&
         }
         const u32 dummy = (PK_P_UNUSED << c.sh) + c.lane;
         const bool w2 = x.wram & x.wr2;
-        c.g[sel(x.wram, x.o0, dummy)] = (u8)x.wv0;
-        c.g[sel(w2, x.o1, dummy)] = (u8)x.wv1;
+        u32 wm = sel(x.wram, ~0u, 0u);   // the store address selects as masks (msel)
+        PK_OPAQUE(wm);
+        const u32 w2m = wm & bmask(m.D, PK_DB_WR2);
+        c.g[msel(wm, x.o0, dummy)] = (u8)x.wv0;
+        c.g[msel(w2m, x.o1, dummy)] = (u8)x.wv1;
         if (x.wram) PK_MEMREF(env, 1u, fast_phys(x.addr0));
         if (w2) PK_MEMREF(env, 1u, fast_phys(x.addr1));
         if (PK_RARE(x.wram & near_hcode(x.addr0))) {
@@ -821,7 +825,7 @@ __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc&
         }
     }
     PK_STAMP_AT(2);
-    if (PK_RARE(x.wr & !x.wram)) {  // rare: IO registers / MBC / SRAM / OAM DMA / IE
+    if (PK_RARE(x.slow)) {  // rare: IO registers / MBC / SRAM / OAM DMA / IE
         St t = s;
         pk_write_slow(&A, c.g, c.lane, c.loc, env, c.gid, &t, x.addr0, x.wv0, x.addr1, x.wv1, x.wr2 ? 1u : 0u,
                       bit(m.U, PK_US_HIFIRST));
@@ -1060,7 +1064,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         Ex x;
         pk_exec<PRIO, ALL>(s, c, pc, bytes, m, ev, x PK_STAMP_ARGS);
         u32 cycles = x.cycles;
-        const bool wr = x.wr, wram = x.wram;
+        const bool wr = x.wr, slow = x.slow;
         // ---------------- fused secondary op (pk_ucode.h pk_u2_entry) ----------------
         // The instruction after this one, if it is a JR (cc), LD r,r', INC/DEC r, INC/DEC BC/DE/HL or
         // NOP, runs in this iteration on the registers and flags just written, as PyBoy's next
@@ -1082,7 +1086,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
             const bool ramok = (pc < 0x8000u) | (!wr & !(pc - 0xFEFEu < 0x82u));
             // next LCD event / LCD-off frame end, 0 with the timer on (tick_lim)
             // (s.lim also bounds the watchdog: clock + cycles < lim implies cycles < slack)
-            const bool fuse = (s.clock + cycles < s.lim) & !(wr & !wram) & ramok & lenok;
+            const bool fuse = (s.clock + cycles < s.lim) & !slow & ramok & lenok;
             const u32 M2 = sel(fuse, u2.y, PK_U2_NONE_Y);
             // X (pair, or register in byte 0); Y = register | immediate n, ^ the subtract mask, + delta;
             // one adder X + Y + carry-in (ADC/SBC: F.C; SUB/SBC/CP: ^ 1), a logic unit (AND XOR OR),
@@ -1114,7 +1118,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
             ev |= sel(fuse, PK_EV_FUSE, 0u);
 #ifdef PK_DBG_FUSE
             ev |= sel(len2 != 0u, 1u << 23, 0u) | sel((int)cycles < slack, 1u << 24, 0u) | sel(s.clock + cycles < s.lim, 1u << 25, 0u)
-                | sel(!(wr & !wram) & ramok, 1u << 27, 0u);
+                | sel(!slow & ramok, 1u << 27, 0u);
 #endif
             s.w0 = w0f;
             s.w1 = w1f;
@@ -1164,7 +1168,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
             // code in a switchable bank not staged in LDS (most of a 64-bank cartridge's banks): two
             // dwords of the global ROM (L2-resident), so the microcode entry is still prefetched here
             // and its LDS latency overlaps the timer/LCD stage like that of staged code
-            const bool fg = nfg & !(wr & !wram);   // unchanged bank (no slow write) and still unstaged
+            const bool fg = nfg & !slow;   // unchanged bank (no slow write) and still unstaged
             pbytes = sel(fg, __builtin_amdgcn_alignbyte(ng1, ng0, nga & 3u), pbytes);
             const u32 op = pbytes & 0xFFu;
             PK_STAMP_AT(4);
