@@ -616,8 +616,9 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     const u32 tkm = (u32)__builtin_amdgcn_sbfe((int)(F | 0x100u), (D >> PK_DB_CPOS) & 15u, 1u) ^ bmask(D, PK_DB_CINV);
     u32 addr0 = 0, addr1 = 0, o0 = 0, o1 = 0;
     bool pair = false, fast01 = false;
-    // operand pools: registers (w1:w0) and ext (q1:q0) = instruction bytes, m0|m1 and SP
-    const u32 asrc = perm(w1, w0, m.AR) | perm(sp << 16, bytes, m.AE);
+    // operand pools: registers (w1:w0) and ext (q1:q0) = instruction bytes, m0|m1 and SP; the
+    // address's ext pool is (SP : instruction bytes) (pk_ucode.h PK_A_SP)
+    const u32 asrc = perm(w1, w0, m.AR) | perm(sp, bytes, m.AE);
     {
         addr0 = (asrc + (u32)sfield(D, PK_DB_AOFF, 2)) & 0xFFFFu;
         addr1 = (addr0 + (u32)sfield(D, PK_DB_ADIR, 2)) & 0xFFFFu;

@@ -67,8 +67,8 @@ enum { PK_UE_D = 0, PK_UE_U, PK_UE_K, PK_UE_V, PK_UE_XR, PK_UE_XE, PK_UE_YR, PK_
 #define PK_DB_AHN 8       // (builder only) immediate address 0xFF00|n
 #define PK_DB_AOFF 9      // 2 bits signed: addr0 = src + aoff
 #define PK_DB_ADIR 11     // 2 bits signed: addr1 = addr0 + adir
-#define PK_DB_CYC 13      // 3 bits cycles/4
-#define PK_DB_XCYC 16     // 2 bits extra cycles/4 when the condition holds
+#define PK_DB_CYC 13      // 3 bits cycles/4 (the kernel reads them pre-scaled from the V word)
+#define PK_DB_XCYC 16     // 2 bits extra cycles/4 when the condition holds (likewise)
 #define PK_DB_CPOS 18     // 4 bits: condition = bit cpos of (F | 0x100)
 #define PK_DB_CINV 22     //         ^ cinv
 #define PK_DB_TSRC 23     // 3 bits jump target (builder: PK_T_*; stored: 0 none, 1 X|Y, 2 JR)
@@ -124,6 +124,8 @@ enum { PK_J_NONE = 0, PK_J_XY = 1, PK_J_JR = 2 };  // stored: target = X | Y (op
 // perm selectors over the ext pool (q1:q0): q0 = op | n<<8 | n2<<16, q1 = m0 | m1<<8 | SP<<16;
 // 0x08 = the sign of n replicated
 #define PK_E_SP 0x0C0C0706u
+// the address pool is (SP : q0) (the kernel's first stage has no m0|m1 yet): SP at bytes 4-5
+#define PK_A_SP 0x0C0C0504u
 #define PK_E_M0 0x0C0C0C04u
 #define PK_E_M16 0x0C0C0504u
 #define PK_E_N 0x0C0C0C01u
@@ -560,7 +562,7 @@ static inline void pk_store_uop(uint32_t* e, PkUop o, bool real) {
     if (o.u & pk_fld(1, PK_UB_YIMM)) ye = (o.u & pk_fld(1, PK_UB_SEXT)) ? PK_E_SEXTN : (o.u & pk_fld(1, PK_UB_IMM8)) ? PK_E_N : PK_E_NN;
     else if (o.u & pk_fld(1, PK_UB_YMEM)) ye = rd2 ? PK_E_M16 : PK_E_M0;
     else if (o.d & pk_fld(1, PK_DB_YSP)) ye = PK_E_SP;
-    if (o.d & pk_fld(1, PK_DB_ASP)) ae = PK_E_SP;
+    if (o.d & pk_fld(1, PK_DB_ASP)) ae = PK_A_SP;
     else if (o.d & pk_fld(1, PK_DB_AIMM)) ae = (o.d & pk_fld(1, PK_DB_AHN)) ? PK_E_HN : PK_E_NN;
     e[PK_UE_D] = o.d & ~(pk_fld(1, PK_DB_ASP) | pk_fld(1, PK_DB_AIMM) | pk_fld(1, PK_DB_AHN) | pk_fld(1, PK_DB_YSP));
     if ((o.d & pk_fld(1, PK_DB_RD)) && !rd2) e[PK_UE_D] |= pk_fld(1, PK_DB_RD1);
