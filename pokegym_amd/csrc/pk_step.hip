@@ -89,8 +89,10 @@ enum {
     PK_EV_RD_WRAM = 1u << 28, PK_EV_WR_WRAM = 1u << 29, PK_EV_WR_VRAM = 1u << 30, PK_EV_WR_HI = 1u << 31
 };
 
-// LDS, staged by each workgroup at kernel entry
-__shared__ __attribute__((aligned(16))) u32 lds_uc[PK_UC_WORDS];                  // microcode + secondary ops
+// LDS, staged by each workgroup at kernel entry: one struct, so the layout is fixed — the ROM bytes
+// first, at LDS address 0, so the fetch's ds_read2_b32 (8-bit dword offsets) takes the byte index
+// as its address with no base add; the microcode reads fold the ROM array's size into their 16-bit
+// offsets (small-LDS kernel; the whole-CU kernel's ROM is larger than the offset field)
 // ROM banks (+ fetch overrun pad), then the HRAM code mirror (below): one byte array, so the
 // next instruction's bytes come from one ds_read2_b32 whichever of the two holds them.
 // Fetch-only mirror of the first PK_HC_ROWS bytes of HRAM (0xFF80-0xFF9F: where games put the
@@ -98,14 +100,24 @@ __shared__ __attribute__((aligned(16))) u32 lds_uc[PK_UC_WORDS];                
 // at PK_HC_BASE + local env * PK_HC_STRIDE, + one dummy byte: the OAM-DMA wait loop runs from HRAM,
 // and fetching it from the HBM image put a second dependent HBM round trip (fetch, then data) into
 // ~30 % of wave iterations.  Code elsewhere in HRAM is fetched from the image.  Data reads/writes
-// stay on the image (authoritative); every HRAM write also updates the mirror (lanes that do not
-// write a mirrored byte store to the dummy byte, so the store needs no branch).  Up to 512 envs per
-// workgroup: 64-env waves two per SIMD when a launch has the envs for it (>= 131,072).
+// stay on the image (authoritative); a plain-RAM write near the mirrored bytes also updates the
+// mirror (near_hcode, a rare branch; the second byte of a one-byte write goes to the dummy byte).
+// Up to 512 envs per workgroup: 64-env waves two per SIMD when a launch has the envs for it
+// (>= 131,072).
 #define PK_HC_ROWS 32u
 #define PK_HC_STRIDE 36u
 #define PK_HC_BASE (PK_LDS_SLOTS * 0x4000u + 16u)
-__shared__ __attribute__((aligned(16))) u8 lds_rom[PK_HC_BASE + PK_WG_ENVS * PK_HC_STRIDE];
-__shared__ int8_t lds_slot[128];                                                  // bank -> slot
+struct PkLds {
+    u8 rom[PK_HC_BASE + PK_WG_ENVS * PK_HC_STRIDE];   // ROM slots, then the HRAM mirror (a multiple of 16 B)
+    u32 u2[PK_UC_WORDS - PK_UC_U2];                   // secondary ops (small-LDS kernel: base in the 16-bit offset)
+    u32 uc[PK_UC_U2];                                 // microcode
+    int8_t slot[128];                                 // bank -> slot
+};
+__shared__ __attribute__((aligned(16))) PkLds pk_lds;
+#define lds_rom pk_lds.rom
+#define lds_uc pk_lds.uc
+#define lds_u2 pk_lds.u2
+#define lds_slot pk_lds.slot
 
 // ---------------------------------------------------------------------------------------------
 // branch-free helpers: arguments are evaluated unconditionally, so ?: on them is a v_cndmask
@@ -130,6 +142,9 @@ __device__ __forceinline__ u32 cpu_sync_pend(u32 cpu) {
 // block copy's batch loads past the copy's end, whose stores are skipped) made the common path wait
 // for vmcnt(0) — i.e. for the previous iteration's byte stores — before issuing its operand read,
 // every iteration.  Draining on the rare path keeps the store acknowledgements off the common path.
+#ifndef PK_ULDS
+#define PK_ULDS 0    // the next instruction's bytes by one unaligned LDS dword read (A/B variant)
+#endif
 #ifndef PK_BF
 #define PK_BF 1      // branch-free image stores in the unstaged-bank instance (pk_write)
 #endif
@@ -740,7 +755,7 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
     // JP/CALL/INT nn, JP HL, RET, RST: X | Y (one of them is 0); JR: pc + 2 + (Y = sext e)
     s.pc = pcn;
     {
-        const u32 tgt = (X + Y + (pcn & m.V)) & 0xFFFFu;
+        const u32 tgt = (X + Y + (pcn & (m.YC >> 16))) & 0xFFFFu;
         const u32 jump = bmask(U, PK_US_JUMP) & tkm;
         s.pc = msel(jump, tgt, pcn);
         ev |= sel(jump != 0u, PK_EV_JUMP, 0u);
@@ -855,7 +870,8 @@ __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc&
 #endif
 template <bool PRIO, bool ALL>
 __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) {
-    for (u32 i = threadIdx.x; i < PK_UC_WORDS; i += blockDim.x) lds_uc[i] = A.ucode[i];
+    for (u32 i = threadIdx.x; i < PK_UC_U2; i += blockDim.x) lds_uc[i] = A.ucode[i];
+    for (u32 i = threadIdx.x; i < PK_UC_WORDS - PK_UC_U2; i += blockDim.x) lds_u2[i] = A.ucode[PK_UC_U2 + i];
     for (u32 i = threadIdx.x; i < 128u; i += blockDim.x) lds_slot[i] = A.bank_slot[i];
     for (u32 sl = 0; sl < A.nslots; sl++) {
         const uint4* src = reinterpret_cast<const uint4*>(A.rom + (size_t)A.slot_bank[sl] * 0x4000u);
@@ -940,7 +956,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
     // flush_lines, K2's blank-screen path — clears its flag)
     s.render = (A.render_last && frame + 1u == A.frames) ? 1u : 0u;
     const uint4* ucv = reinterpret_cast<const uint4*>(lds_uc);
-    const uint4* ucv2 = reinterpret_cast<const uint4*>(lds_uc + PK_UC_U2);
+    const uint4* ucv2 = reinterpret_cast<const uint4*>(lds_u2);
     const u32* romw = reinterpret_cast<const u32*>(lds_rom);
 
     int slack = (int)(16u * FRAME_CYCLES);  // frame watchdog: PK_FRAME_BUDGET - budget (oracle/gbcore.c)
@@ -1058,8 +1074,10 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         const Mc m = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y, e2.z, e2.w, e3.x, e3.y, e3.z, e3.w};
         const u32 D = m.D;
         // the successor's secondary-op entry (read now: its LDS latency overlaps the execute stage)
-        const u32 nxt = bytes >> (8u * (D & 3u));
-        const u32 i2 = min((nxt & 0xFFu) | (D & (1u << PK_DB_NOFUSE)), PK_U2_NONE);
+        // (nxt: byte 0 the successor's opcode — 0xFF, never a secondary op, after a primary that may
+        // not fuse — byte 1 its operand: one v_perm with the entry's selector, pk_ucode.h V word)
+        const u32 nxt = perm(bytes, bytes, m.V);
+        const u32 i2 = nxt & 0xFFu;
         const uint4 u2 = ucv2[2u * i2], u2b = ucv2[2u * i2 + 1u];
         // ---------------- execute ----------------
         Ex x;
@@ -1164,13 +1182,18 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
             // staged ROM or the HRAM code mirror: one LDS byte index, one ds_read2_b32
             const bool fh = npc - 0xFF80u < PK_HC_ROWS - 2u;
             const u32 la = sel(fh, PK_HC_BASE + c.loc * PK_HC_STRIDE + (npc - 0xFF80u), sel(fl, rom_lds_index(s, npc), 0u));
+#if PK_ULDS
+            // one unaligned ds_read_b32 (the driver runs gfx9 LDS in unaligned mode)
+            pbytes = *reinterpret_cast<const u32*>(lds_rom + la);
+#else
             const u32 r0 = romw[la >> 2], r1 = romw[(la >> 2) + 1u];
-            pbytes = __builtin_amdgcn_alignbyte(r1, r0, la & 3u);
+            pbytes = __builtin_amdgcn_alignbyte(r1, r0, la);   // (v_alignbyte_b32 takes the shift's low 2 bits)
+#endif
             // code in a switchable bank not staged in LDS (most of a 64-bank cartridge's banks): two
             // dwords of the global ROM (L2-resident), so the microcode entry is still prefetched here
             // and its LDS latency overlaps the timer/LCD stage like that of staged code
             const bool fg = nfg & !slow;   // unchanged bank (no slow write) and still unstaged
-            pbytes = sel(fg, __builtin_amdgcn_alignbyte(ng1, ng0, nga & 3u), pbytes);
+            pbytes = sel(fg, __builtin_amdgcn_alignbyte(ng1, ng0, nga), pbytes);
             const u32 op = pbytes & 0xFFu;
             PK_STAMP_AT(4);
             const u32 di = sel(op == 0xCBu, 256u + ((pbytes >> 8) & 0xFFu), op);

@@ -23,9 +23,12 @@ enum { PK_UE_D = 0, PK_UE_U, PK_UE_K, PK_UE_V, PK_UE_XR, PK_UE_XE, PK_UE_YR, PK_
        PK_UE_S0, PK_UE_S1, PK_UE_YC, PK_UE_YX, PK_UE_CW, PK_UE_CI, PK_UE_WORDS };
 // stored words (what the kernel reads; the builder below works in the PK_UB_/PK_KB_ form):
 //   U  datapath control bits PK_US_*          K  FC | FK << 8 | FM << 16 | CPUAND << 24 | CPUOR << 28
-//   V  0xFFFF for JR (target = pc + len + Y), else 0; | cycles << 16 | extra cycles when the
-//      condition holds << 24 (the D fields CYC/XCYC times 4: one add and one select in the kernel)
-//   YC Y constant (INC/DEC, CPL, BIT/RES/SET masks, RST vector)   YX 0x1FFFF when the adder subtracts
+//   V  the successor selector: bytes 0-1 = a v_perm selector taking the fetched bytes' successor
+//      opcode and operand (bytes len, len + 1), or 0xFF (0x0D: RST 38h, no secondary op) for a
+//      primary that may not fuse; | cycles << 16 | extra cycles when the condition holds << 24 (the D
+//      fields CYC/XCYC times 4: one add and one select in the kernel)
+//   YC Y constant (INC/DEC, CPL, BIT/RES/SET masks, RST vector); bits 16-31: 0xFFFF for JR (target =
+//      pc + len + Y; Y's bits above 16 reach no result)                YX 0x1FFFF when the adder subtracts
 //   CW/CI carry-in (adder) / shifted-in bit (right-shift unit) = bit CW of (X | F << 16) ^ CI:
 //         bit 20 = F.C, bit 7/bit 0 = X's top/bottom bit, bit 16 = constant 0 (with CI: constant 1)
 #define PK_US_LOGIC 0     // result8 from the logic unit (loads: X = 0xFF AND Y), else adder / right unit
@@ -47,10 +50,9 @@ enum { PK_UE_D = 0, PK_UE_U, PK_UE_K, PK_UE_V, PK_UE_XR, PK_UE_XE, PK_UE_YR, PK_
 #define PK_UC_INT 512u    // pseudo-op: interrupt dispatch (push PC, jump to the vector)
 #define PK_UC_IDLE 513u   // pseudo-op: halted / crashed CPU, 4 cycles
 #define PK_UC_NOP0 514u   // pseudo-op: interrupt pending with IME off (queued), 0 cycles
-// secondary-op table (fused pairs, see pk_u2_entry): 257 entries x 8 dwords after the main table
-// (entry 256 is empty: the index of every primary that may not fuse)
+// secondary-op table (fused pairs, see pk_u2_entry): 256 entries x 8 dwords after the main table
 #define PK_U2_WORDS 8u
-#define PK_U2_NONE 256u
+#define PK_U2_NONE 0xFFu   // RST 38h: never a secondary op (the index of every primary that may not fuse)
 #define PK_UC_U2 (PK_UC_ENTRIES * PK_UE_WORDS)
 #define PK_UC_WORDS (PK_UC_U2 + (PK_U2_NONE + 1u) * PK_U2_WORDS)
 
@@ -573,7 +575,9 @@ static inline void pk_store_uop(uint32_t* e, PkUop o, bool real) {
         e[PK_UE_D] |= pk_fld(1, PK_DB_NOFUSE);
     e[PK_UE_U] = us;
     e[PK_UE_K] = fconst | (fkeep << 8) | (fm << 16) | (cpu_keep << 24) | (cpu_set << 28);
-    e[PK_UE_V] = jrm | ((((o.d >> PK_DB_CYC) & 7u) * 4u) << 16) | ((((o.d >> PK_DB_XCYC) & 3u) * 4u) << 24);
+    const uint32_t len = o.d & 3u;
+    const uint32_t succ = (e[PK_UE_D] & pk_fld(1, PK_DB_NOFUSE)) ? 0x0C0Du : (len | ((len + 1u) << 8));
+    e[PK_UE_V] = succ | ((((o.d >> PK_DB_CYC) & 7u) * 4u) << 16) | ((((o.d >> PK_DB_XCYC) & 3u) * 4u) << 24);
     e[PK_UE_XR] = xe != PK_PZERO ? PK_PZERO : o.px;
     e[PK_UE_XE] = xe;
     e[PK_UE_YR] = ye != PK_PZERO ? PK_PZERO : o.py;
@@ -582,7 +586,7 @@ static inline void pk_store_uop(uint32_t* e, PkUop o, bool real) {
     e[PK_UE_AE] = ae;
     e[PK_UE_S0] = o.s0;
     e[PK_UE_S1] = o.s1;
-    e[PK_UE_YC] = yc;
+    e[PK_UE_YC] = yc | (jrm << 16);
     e[PK_UE_YX] = yx;
     e[PK_UE_CW] = cw;
     e[PK_UE_CI] = ci;

@@ -50,7 +50,6 @@ static inline uint32_t __builtin_amdgcn_perm(uint32_t hi, uint32_t lo, uint32_t 
     }
     return r;
 }
-// v_alignbyte_b32: ({hi, lo} >> (8 * (sh & 3)))[31:0]
 // v_bfe_u32: width bits at offset (both & 31); width 0 -> 0
 static inline uint32_t __builtin_amdgcn_ubfe(uint32_t src, uint32_t off, uint32_t width) {
     off &= 31u;
@@ -67,6 +66,7 @@ static inline int __builtin_amdgcn_sbfe(int src, uint32_t off, uint32_t width) {
     if (off + width >= 32u) return (int)src >> off;
     return (int)((uint32_t)src << (32u - off - width)) >> (32u - width);
 }
+// v_alignbyte_b32: ({hi, lo} >> (8 * (sh & 3)))[31:0]
 static inline uint32_t __builtin_amdgcn_alignbyte(uint32_t hi, uint32_t lo, uint32_t sh) {
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (sh & 3)));
 }
