@@ -142,9 +142,6 @@ __device__ __forceinline__ u32 cpu_sync_pend(u32 cpu) {
 // block copy's batch loads past the copy's end, whose stores are skipped) made the common path wait
 // for vmcnt(0) — i.e. for the previous iteration's byte stores — before issuing its operand read,
 // every iteration.  Draining on the rare path keeps the store acknowledgements off the common path.
-#ifndef PK_ULDS
-#define PK_ULDS 0    // the next instruction's bytes by one unaligned LDS dword read (A/B variant)
-#endif
 #ifndef PK_BF
 #define PK_BF 1      // branch-free image stores in the unstaged-bank instance (pk_write)
 #endif
@@ -1182,13 +1179,10 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
             // staged ROM or the HRAM code mirror: one LDS byte index, one ds_read2_b32
             const bool fh = npc - 0xFF80u < PK_HC_ROWS - 2u;
             const u32 la = sel(fh, PK_HC_BASE + c.loc * PK_HC_STRIDE + (npc - 0xFF80u), sel(fl, rom_lds_index(s, npc), 0u));
-#if PK_ULDS
-            // one unaligned ds_read_b32 (the driver runs gfx9 LDS in unaligned mode)
-            pbytes = *reinterpret_cast<const u32*>(lds_rom + la);
-#else
+            // (one unaligned ds_read_b32 instead — the LDS runs in unaligned mode — measured ±0.5 %:
+            // profiles/r05/ab_diet r05m; not kept, as it would rest on a driver setting)
             const u32 r0 = romw[la >> 2], r1 = romw[(la >> 2) + 1u];
             pbytes = __builtin_amdgcn_alignbyte(r1, r0, la);   // (v_alignbyte_b32 takes the shift's low 2 bits)
-#endif
             // code in a switchable bank not staged in LDS (most of a 64-bank cartridge's banks): two
             // dwords of the global ROM (L2-resident), so the microcode entry is still prefetched here
             // and its LDS latency overlaps the timer/LCD stage like that of staged code
