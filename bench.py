@@ -505,7 +505,8 @@ def main():
                                    "LDS fetch -> microcode -> address -> operand-read chain of its divergent lanes and the "
                                    "fused datapath; with two waves per SIMD the SIMD's other wave covers the chain's "
                                    "latency (requesting the operand ~50 instructions earlier saved nothing, "
-                                   "profiles/r05/ab_pre), so instruction cuts are what move the rate; a lone wave "
+                                   "profiles/r05/ab_pre), so instruction cuts are what move the rate (round 5: 398 -> 340 issued per "
+                                   "iteration, every step A/B'd, profiles/r05/ab_diet); a lone wave "
                                    "(config2) is ~70 % issue; a launch lasts as long as its slowest wave (an env in a "
                                    "long LCD-off map load: kernel ~1.35x the mean wave, profiles/r03_wavetime).  `issue` "
                                    "carries the PMC ISA counts per emulated instruction; `frac` is only the HBM price of "
