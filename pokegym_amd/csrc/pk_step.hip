@@ -673,7 +673,17 @@ __device__ __forceinline__ void pk_exec(St& s, const Ctx& c, u32 pc, u32 bytes, 
         if (rrom) om = lds_rom[rom_lds_index(s, addr0)];
         if (PK_RARE(rd & !rram & !rrom)) {  // rare: IO registers (LY, STAT, joypad, ...), SRAM, unstaged ROM, DAA
             PK_STAMP_AT(0);
-            if (bit(D, PK_DB_DAA)) {
+            // DIV first, on its own: the RNG's source (pokered's Random; pkbench reads it in a quarter
+            // of all wave iterations) — a wave whose rare lanes all read DIV skips the bus dispatch
+            if ((addr0 == 0xFF04u) & !rd2) {
+                om = bfe8(s.divacc, 8);
+                PK_MEMREF(c.env, 2u, addr0);
+                ev |= PK_EV_RD_IO;
+            } else if ((addr0 == 0xFF00u) & !rd2) {   // JOYP, next (its image byte: o0 = PK_P_IO)
+                om = c.g[o0];
+                PK_MEMREF(c.env, 2u, addr0);
+                ev |= PK_EV_RD_IO;
+            } else if (bit(D, PK_DB_DAA)) {
                 // DAA (opcodes.py DAA_27): its microcode reads two bytes at 0xFFFF (IE: never a fast
                 // or staged read) to land here, and takes the result as POP AF takes m1|m0: A = m1,
                 // F = m0 & 0xF0 — so the common path carries no DAA test of its own
