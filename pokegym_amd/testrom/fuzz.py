@@ -253,6 +253,51 @@ def hram_code_rom(n_banks: int = 2) -> bytes:
     return build_rom("\n".join(L), n_banks=n_banks, title="HRAMCODE")
 
 
+def io_edge_rom(n_banks: int = 2) -> bytes:
+    """The IO accesses K1 serves first inside its rare branches (pk_step.hip: one-byte DIV and JOYP
+    reads, one-byte sound and JOYP writes) beside the forms that must still take the general bus:
+    16-bit reads and writes at the same addresses (pop / push / ld [a16],sp, one of each across
+    the sound block's end into LCDC), read-modify-write instructions on DIV, JOYP and NR52,
+    [c]-relative and absolute addressing, a JOYP select that changes every pass and a DIV reset
+    every 8th pass.  Every value read is summed into WRAM each pass (so a wrong read in any pass
+    shows in the final image), and the last pass's values stay at 0xC010-0xC022."""
+    L = ["section 0", "org $0040", "reti", "org $0048", "reti", "org $0050", "reti", "org $0058", "reti",
+         "org $0060", "reti", "org $0100", "nop", "jp start", "org $0150",
+         "start:", "di", "ld sp, $dff0", "ld a, $e3", "ldh [$40], a", "ld b, 0",
+         "ld a, $05", "ldh [$07], a",                               # the timer runs (TIMA next to DIV)
+         "main:",
+         # JOYP: the select bits change per pass; one-byte reads by ldh, [c] and through HL
+         "ld a, b", "swap a", "and $30", "ldh [$00], a", "ldh a, [$00]", "ldh a, [$00]", "ld e, a",
+         "ld [$c010], a", "call acc",
+         "ld a, b", "or $a5", "ldh [$01], a",                      # SB: JOYP's neighbour in a 16-bit read
+         "ld a, $20", "ldh [$00], a", "ld c, $00", "ldh a, [c]", "ld [$c011], a", "call acc",
+         "ld hl, $ff00", "set 4, [hl]", "ld a, [hl]", "ld [$c012], a", "call acc",
+         # DIV: ldh, absolute and HL reads; a reset by a read-modify-write every 8th pass
+         "ldh a, [$04]", "ld [$c013], a", "call acc",
+         "ld a, [$ff04]", "ld [$c014], a", "call acc",
+         "ld hl, $ff04", "ld a, [hl]", "ld [$c015], a", "call acc",
+         "ld a, b", "and $07", "jr nz, .nodiv", "inc [hl]", ".nodiv:",
+         # sound (not emulated): one-byte writes and reads, a read-modify-write of NR52
+         "ld a, e", "ldh [$24], a", "ldh [$25], a", "ld [$ff30], a", "ldh [$3f], a",
+         "ldh a, [$25]", "ld [$c016], a", "call acc",
+         "ldh a, [$30]", "ld [$c017], a", "call acc",
+         "ld hl, $ff26", "inc [hl]", "ld a, [hl]", "ld [$c018], a", "call acc",
+         # 16-bit accesses: a push into NR10/NR11, pops across FF03/DIV and DIV/TIMA, JOYP/SB and NR52's block end
+         # into LCDC, and ld [a16],sp across FF3F/LCDC (SP's high byte lands in LCDC, read back, restored)
+         "ld d, b", "ld sp, $ff12", "push de", "ld sp, $ff03", "pop hl", "ld sp, $ff00", "pop de",
+         "ld sp, $ff3f", "pop bc", "ld sp, $e7e0", "ld [$ff3f], sp", "ld sp, $dff0",
+         "ldh a, [$40]", "ld [$c01e], a", "call acc", "ld a, $e3", "ldh [$40], a",
+         "ld a, l", "ld [$c019], a", "call acc", "ld a, h", "ld [$c01a], a", "call acc",
+         "ld a, e", "ld [$c01b], a", "call acc", "ld a, d", "ld [$c01c], a", "call acc",
+         "ld a, c", "ld [$c01d], a", "call acc", "ld a, b", "call acc",
+         "ld sp, $ff04", "pop hl", "ld sp, $dff0",                 # DIV + TIMA as one 16-bit read
+         "ld a, l", "ld [$c021], a", "call acc", "ld a, h", "ld [$c022], a", "call acc",
+         "ld a, [$c020]", "inc a", "ld [$c020], a", "ld b, a",
+         "jp main",
+         "acc:", "push hl", "ld hl, $c01f", "add a, [hl]", "ld [hl], a", "pop hl", "ret"]
+    return build_rom("\n".join(L), n_banks=n_banks, title="IOEDGE")
+
+
 def copydata_rom() -> bytes:
     """pokered's CopyData loop (home/copy.asm) and its B/C-swapped twin — which K1 runs in blocks of
     whole passes (pk_step.hip pk_copy_loop) — called with per-env parameters from the joypad and an

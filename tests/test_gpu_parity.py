@@ -210,6 +210,19 @@ def test_hram_code_parity_64_banks():
     assert not bad, bad[:4]
 
 
+@pytest.mark.parametrize("n_banks", [2, 64])
+def test_io_edges_parity(n_banks):
+    """The IO accesses K1 serves first inside its rare branches (one-byte DIV / JOYP reads, sound /
+    JOYP writes) beside 16-bit and read-modify-write accesses at the same addresses, the timer
+    running and JOYP's select changing every pass (fuzz.py io_edge_rom); 2 banks: the every-bank
+    staged instance, 64: the unstaged-bank one."""
+    from pokegym_amd.testrom.fuzz import io_edge_rom
+    n = 256
+    gpu, ref = _run_both(io_edge_rom(n_banks), None, n, 4, 7)
+    bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
+    assert not bad, bad[:4]
+
+
 def warp_actions(n, seed=5):
     """Actions (6, n) from the warp fixture's state: columns 0..n/2-1 the recorded actions (they
     walk through a door at step 2: pkbench's map load with the LCD off for ~5 frames), the rest

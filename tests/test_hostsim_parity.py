@@ -54,6 +54,15 @@ def test_hostsim_hram_code(n_banks):
     assert check(hram_code_rom(n_banks), 8, 3, 5) == []
 
 
+@pytest.mark.parametrize("n_banks", [2, 64])
+def test_hostsim_io_edges(n_banks):
+    """DIV / JOYP reads and sound / JOYP writes — served first inside K1's rare branches — beside
+    16-bit and read-modify-write accesses at the same addresses (pokegym_amd/testrom/fuzz.py
+    io_edge_rom); 64 banks: the unstaged-bank instance."""
+    from pokegym_amd.testrom.fuzz import io_edge_rom
+    assert check(io_edge_rom(n_banks), 8, 3, 7) == []
+
+
 def test_hostsim_frame_watchdog():
     """The frame watchdog: LCD switched off faster than once per frame (its clock restarts, so
     frames end on the budget), joypad-dependent passes, timer stretches with TIMA interrupts
