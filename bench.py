@@ -105,9 +105,10 @@ def _cpu_baseline(rom: bytes, state, seconds_target: float = 10.0):
     Two shapes on whatever cores the box grants: the reference's own CPU shape, 72 envs each in its
     own worker (README.md:116-118; PufferLib multiprocessing), and a run sized to the box's CPU share
     (cgroup quota, else the 16 threads the GPU box allots one GPU: OMP_NUM_THREADS) with 4 envs per
-    worker.  `value` is the reference's shape (72 one-env workers, as BASELINE's CPU path runs); the
-    share-sized run is recorded beside it (`share_sized_run`, and `best_value` = the faster of the
-    two), with the worker count beside `cores`.  Plus the workload intensity of the action stream."""
+    worker.  `value` is the STRONGER of the two measured CPU figures (the denominator of any GPU/CPU
+    ratio is the best CPU number this box produced; round 5 reported the 72-worker shape instead,
+    ~1.3x lower); both runs are recorded beside it (`reference_shape_run`, `share_sized_run`) with
+    `shape`/`workers` naming the one `value` is.  Plus the workload intensity of the action stream."""
     from oracle import oracle
     oracle.lib()
     try:
@@ -127,20 +128,23 @@ def _cpu_baseline(rom: bytes, state, seconds_target: float = 10.0):
     steps_s = max(4, int(seconds_target / 4 / per_step))
     vs, walls, ipss = _cpu_run(rom, state, share, 4, steps_s, 1000)
     inten = oracle.intensity(rom, state, 128, 3, 16, 99)   # 2,048 env-steps of the same action stream
+    share_best = vs >= v72
     return {
-        "value": round(v72, 1),
+        "value": round(max(v72, vs), 1),
         "unit": "env-steps/s",
         "cores": share,
-        "workers": 72,
+        "workers": share if share_best else 72,
         "kind": "port",
-        "shape": "72-worker reference shape (README.md:116-118)",
+        "shape": (f"share-sized run ({share} workers x 4 envs), the faster of the two" if share_best
+                  else "72-worker reference shape (README.md:116-118), the faster of the two"),
         "best_value": round(max(v72, vs), 1),
         "sample": (f"the C oracle (oracle/gbcore.c, 1 thread per worker) on a CPU share of {share} cores "
                    f"({'cgroup ' + quota_raw if quota else 'no cgroup quota; OMP_NUM_THREADS=' + str(omp or 'unset') + ' is the box share'}), "
-                   f"same ROM and random-action stream; value = the reference's CPU shape, 72 one-env workers "
-                   f"(README.md:116-118) x {steps72} timed env-steps; beside it (share_sized_run, best_value) {share} "
+                   f"same ROM and random-action stream; two runs: the reference's CPU shape, 72 one-env workers "
+                   f"(README.md:116-118) x {steps72} timed env-steps, and {share} "
                    f"workers x 4 envs x {steps_s} "
-                   "timed env-steps (after 3 warmup each); aggregate over the slowest worker's timed span. Workers are "
+                   "timed env-steps (after 3 warmup each); value = the faster of the two; aggregate over the slowest "
+                   "worker's timed span. Workers are "
                    "threads (ctypes releases the GIL), not forked processes. PyBoy+pokegym itself is not installed "
                    "(pure-Python PyBoy would be slower than this C restatement)"),
         "instr_per_s": round(max(ips72, ipss), 1),

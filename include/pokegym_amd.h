@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PK_ABI_VERSION 5
+#define PK_ABI_VERSION 6
 #define PK_STATE_V9_BYTES 142610u
 #define PK_SCREEN_ROWS 144u
 #define PK_SCREEN_COLS 160u
@@ -164,6 +164,12 @@ int pk_snapshot_range(pk_handle* h, uint32_t env0, uint32_t count, uint8_t* host
 
 /* Emulated instructions executed by the last pk_step, summed over envs (synchronous). */
 int pk_last_instr_count(pk_handle* h, uint64_t* out);
+
+/* The K1 launch shape pk_step_range(h, env0, count, ...) takes (host-side, no GPU work):
+ * out[0] = 1 for the small-LDS kernel, out[1] = envs per wave, out[2] = threads per workgroup,
+ * out[3] = 1 for the wave-priority variant, out[4] = 1 for the every-bank-staged (ALL) instance.
+ * Lets parity tests assert that they run the benchmarked launch. */
+int pk_launch_shape(pk_handle* h, uint32_t env0, uint32_t count, uint32_t* out5);
 
 /* Kernel timing with HIP events recorded on the step's stream around K1 (emulate), K2 (render)
  * and K4+K3 (reward + obs) of every pk_step while enabled.  pk_profile_read synchronises,

@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # PK_LIB selects an alternative in-tree build (A/B kernel experiments); default: lib/libpokegym_amd.so
 LIB_PATH = os.environ.get("PK_LIB") or os.path.join(HERE, "lib", "libpokegym_amd.so")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 PK_F_RENDER = 1
 PK_F_REWARD = 2
 PK_F_RELOAD_ON_RESET = 4
@@ -31,7 +31,7 @@ EXPORTS = ("pk_create", "pk_destroy", "pk_last_error", "pk_abi_version", "pk_res
            "pk_last_instr_count", "pk_profile_enable", "pk_profile_read", "pk_obs_ptr", "pk_error_ptr",
            "pk_get_ram", "pk_set_ram", "pk_info_ptr", "pk_info_flag_ptr", "pk_info_stride", "pk_heatmap_ptr", "pk_info_bits_ptr",
            "pk_snapshot_range", "pk_render_latched", "pk_step_range", "pk_reset_range",
-           "pk_set_episode_params")
+           "pk_set_episode_params", "pk_launch_shape")
 
 
 class PkConfig(ctypes.Structure):
@@ -93,6 +93,7 @@ def bind(L):
     L.pk_snapshot_range.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u8p, ctypes.c_uint64]
     L.pk_render_latched.argtypes = [vp, vp]
     L.pk_last_instr_count.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
+    L.pk_launch_shape.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
     L.pk_profile_enable.argtypes = [vp, ctypes.c_int]
     dp = ctypes.POINTER(ctypes.c_double)
     L.pk_profile_read.argtypes = [vp, dp, dp, dp, ctypes.POINTER(ctypes.c_uint64)]

@@ -207,7 +207,7 @@ void export_v9(const Template& tp, const uint32_t* regs, const uint8_t* mem, con
     memcpy(s + S_WRAM, mem + PK_P_WRAM, 8192);
     memcpy(s + S_FEA0, mem + PK_P_OAM + 0xA0, 96);
     memcpy(s + S_IO, mem + PK_P_IO, 76);
-    memcpy(s + S_HRAM, mem + PK_P_HRAM, 127);
+    memcpy(s + S_HRAM, mem + PK_P_HRAM, 127);   // 0xFF80-0xFFFE: never phys 0x41FF (PK_P_UNUSED, K1's dummy store)
     memcpy(s + S_FF4C, mem + PK_P_IO + 0x4C, 52);
     uint32_t t0 = regs[PK_R_TIM0], t1 = regs[PK_R_TIM1];
     uint8_t* tm = s + S_TIMER;
@@ -1005,6 +1005,19 @@ int pk_last_instr_count(pk_handle* h, uint64_t* out) {
     uint64_t s = 0;
     for (uint32_t x : v) s += x;
     *out = s;
+    return 0;
+}
+
+int pk_launch_shape(pk_handle* h, uint32_t env0, uint32_t count, uint32_t* out5) {
+    int rc;
+    if (!out5) return fail(-EINVAL, "null argument");
+    if ((rc = check_range(h, env0, count))) return rc;
+    const PkStepArgs a = step_args(h, nullptr, env0, env0 + count);
+    out5[0] = a.small;
+    out5[1] = a.wave_lanes;
+    out5[2] = a.block;
+    out5[3] = a.prio;
+    out5[4] = a.all_staged;
     return 0;
 }
 

@@ -56,7 +56,14 @@ __host__ __device__ static inline uint64_t pk_img_off(uint32_t env, uint32_t phy
 #define PK_P_IO 0x4100u
 #define PK_P_HRAM 0x4180u
 #define PK_P_SRAM 0x4200u
-#define PK_P_UNUSED 0x41FFu   // no guest byte (IE lives in lane regs): K1's dummy store target
+#define PK_P_UNUSED 0x41FFu   // no guest byte (IE lives in lane regs): K1's dummy store target.
+                              // K1's branch-free write stage stores a changing byte here every
+                              // iteration, so nothing may read it: the v9 export/import and every
+                              // image digest cover HRAM as 0x4180-0x41FE only (127 bytes) and take
+                              // IE from the cpu register (pk_capi.cpp export_v9 / import_v9).
+                              // The 64-bank parity tests (test_hostsim_game_64_banks,
+                              // test_game_rom_64_banks_parity) would fail if an export read it: that
+                              // instance stores unmodelled values here in every iteration
 
 #define PK_ROWS 144u
 #define PK_COLS 160u

@@ -61,6 +61,14 @@
 #ifndef PK_ITER_OP
 #define PK_ITER_OP(env, di) ((void)0)
 #endif
+// invariants of the lane-cached derived state (pk_check_lane, run at every loop top): the host-
+// simulation build defines PK_CHECK to record a failure; the gfx950 build compiles the checks away
+#ifdef PK_CHECK
+#define PK_CHECK_ON 1
+#else
+#define PK_CHECK_ON 0
+#define PK_CHECK(env, cond, what) ((void)0)
+#endif
 // diagnostic build only (-DPK_STAMP, tools/stamp_build.py): per-phase wave cycles of the loop,
 // read with s_memtime at points where the loop already waits, summed per wave into A.dbg
 #ifdef PK_STAMP
@@ -877,6 +885,49 @@ __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc&
                               sel(x.addr0 >= 0x8000u && x.addr0 < 0xA000u, PK_EV_WR_VRAM, 0u)), 0u);
 }
 
+#if PK_CHECK_ON
+// The lane state K1 caches instead of recomputing — none of it is stored, so the v9 state cannot
+// show it directly — checked against a recomputation from the architectural state at the top of
+// every iteration (host simulation only; tests/hostsim records the failures and every hostsim run
+// fails on one):
+//   * the CPU_PEND bit == (IE & IF & 0x1F) != 0 (cpu_sync_pend at every IE/IF change);
+//   * lim: 0 while halted or while the timer runs (HALT folded into the tick limit), never past the
+//     next LCD event / LCD-off frame end, never past the watchdog budget (clock + slack) — the
+//     bounds that let the common path skip the timer/LCD stage and fuse a second instruction;
+//   * rb / rlim == the staged slot of the current ROM bank;
+//   * the HRAM code mirror == the image's bytes 0xFF80-0xFF9F;
+//   * prefetched bytes (pbytes != PK_COPY_W0) == the bytes the bus holds at pc (the ones any use can
+//     take: up to the bank end for ROM code, 3 for code in RAM) and p0..p3 == their microcode entry.
+static __device__ void pk_check_lane(const St& s, const Ctx& c, int slack, u32 pbytes, const uint4& p0, const uint4& p1,
+                              const uint4& p2, const uint4& p3) {
+    const u32 env = c.env, cpu = s.cpu;
+    PK_CHECK(env, ((cpu & CPU_PEND) != 0u) == (((cpu >> 8) & (cpu >> 16) & 0x1Fu) != 0u), "CPU_PEND != IE & IF");
+    PK_CHECK(env, !(cpu & CPU_HALT) || s.lim == 0u, "halted with lim != 0");
+    PK_CHECK(env, !(s.tim0 & (4u << 24)) || s.lim == 0u, "timer on with lim != 0");
+    PK_CHECK(env, s.lim <= sel(s.lcd0 & 0x80u, s.target, FRAME_CYCLES), "lim past the next LCD event / frame end");
+    PK_CHECK(env, (long long)s.lim <= (long long)s.clock + slack, "lim past the watchdog budget");
+    const u32 base = slot_base((s.mbc & 0xFFu) & c.A->rom_bank_mask);
+    PK_CHECK(env, s.rlim == sel(base != PK_NO_BANK, 0x8000u, 0x4000u), "rlim != staged(bank)");
+    PK_CHECK(env, base == PK_NO_BANK || s.rb == base - 0x4000u, "rb != slot(bank)");
+    for (u32 i = 0; i < PK_HC_ROWS; i++)
+        PK_CHECK(env, lds_rom[PK_HC_BASE + c.loc * PK_HC_STRIDE + i] == ld_img(c, PK_P_HRAM + i), "HRAM code mirror stale");
+    if (pbytes != PK_COPY_W0) {
+        const u32 pc = s.pc;
+        const u32 nb = pc < 0x8000u ? min(4u, 0x4000u - (pc & 0x3FFFu)) : 3u;
+        for (u32 k = 0; k < nb; k++)
+            PK_CHECK(env, ((pbytes >> (8u * k)) & 0xFFu) == bus_read_any(c, s, (pc + k) & 0xFFFFu), "prefetched bytes stale");
+        const u32 op = pbytes & 0xFFu;
+        const u32 di = op == 0xCBu ? 256u + ((pbytes >> 8) & 0xFFu) : op;
+        const uint4* ucv = reinterpret_cast<const uint4*>(lds_uc);
+        const uint4 q[4] = {p0, p1, p2, p3};
+        for (u32 k = 0; k < 4u; k++) {
+            const uint4 e = ucv[di * 4u + k];
+            PK_CHECK(env, e.x == q[k].x && e.y == q[k].y && e.z == q[k].z && e.w == q[k].w, "prefetched microcode stale");
+        }
+    }
+}
+#endif
+
 // ---------------------------------------------------------------------------------------------
 // K1
 // PRIO: the launch runs two waves per SIMD (A.prio, chosen by the host), and K1 raises a wave's
@@ -993,6 +1044,9 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
 #endif
     while (frame < A.frames) {
         u32 ev = 0;
+#if PK_CHECK_ON
+        pk_check_lane(s, c, slack, pbytes, p0, p1, p2, p3);
+#endif
 #ifdef PK_WAVETIME
         wt_iter++;
 #endif

@@ -598,8 +598,11 @@ static inline void pk_store_uop(uint32_t* e, PkUop o, bool real) {
 // LD r,n, INC/DEC r, INC/DEC BC/DE/HL, an 8-bit ALU op on A with a register or immediate operand
 // (ADD ADC SUB SBC AND XOR OR CP), CPL, SCF or NOP right after a fusable instruction executes on
 // the registers and flags that instruction left, exactly as the next cpu.tick would, when nothing
-// can happen in between (pk_step.hip states the test).  Index = opcode, or PK_U2_NONE (empty) for a
-// primary with PK_DB_NOFUSE.  Entry, two uint4:
+// can happen in between (pk_step.hip states the test).  Index = the successor's opcode (256
+// entries).  A primary with PK_DB_NOFUSE selects index PK_U2_NONE = 0xFF for its successor
+// whatever the bytes (its V word's successor selector yields 0xFF): that index is also RST 38h's
+// own entry, which must therefore stay empty (length 0) — RST is a control transfer, never a
+// secondary op; tests/test_ucode_table.py checks both.  Entry, two uint4:
 //   a.x  X selector over w1:w0 (the pair, or a register into byte 0; JR: the F mask at F's byte)
 //   a.y  misc: length, cycles, delta, JR condition value, mask of the F bits the op writes
 //   a.z/a.w  writeback selectors of val2 = res16 | F' << 16 | res8 << 24 (as S0/S1)

@@ -229,6 +229,14 @@ class BatchedEmulator:
         check(self._L.pk_last_instr_count(self._h, ctypes.byref(v)), "pk_last_instr_count")
         return int(v.value)
 
+    def launch_shape(self, env0: int = 0, count: int | None = None) -> dict:
+        """The K1 launch pk_step_range(env0, count) takes (pk_launch_shape; host-side, no GPU work)."""
+        out = (ctypes.c_uint32 * 5)()
+        count = self.n - env0 if count is None else count
+        check(self._L.pk_launch_shape(self._h, env0, count, out), "pk_launch_shape")
+        return {"small": bool(out[0]), "wave_lanes": int(out[1]), "block": int(out[2]), "prio": bool(out[3]),
+                "all_staged": bool(out[4])}
+
     def profile_enable(self, on: bool = True):
         check(self._L.pk_profile_enable(self._h, 1 if on else 0), "pk_profile_enable")
 

@@ -298,6 +298,52 @@ def io_edge_rom(n_banks: int = 2) -> bytes:
     return build_rom("\n".join(L), n_banks=n_banks, title="IOEDGE")
 
 
+def irq_bank_rom(n_banks: int = 8) -> bytes:
+    """Two paths whose effect K1 caches in lane state instead of re-deriving it every iteration
+    (pk_step.hip pk_check_lane): (1) IF and IE writes — K1 keeps "an interrupt is pending" as a bit
+    of its cpu word, updated wherever IE or IF change — with IME off, read back, then a short IME-on
+    window (ei / nop / nop / di) in which whatever the writes left pending dispatches, the timer
+    raising its own IF bit meanwhile in half of the passes; (2) ROM-bank switches issued from code IN the switchable bank:
+    every bank holds the same routine at 0x4000 that writes the next bank number to the MBC and
+    continues at the next address — fetched from the NEW bank, whose immediate differs — so a fetch
+    prefetched from the old bank before the switch would show in WRAM (K1 refetches after a slow
+    write).  n_banks 8: the switch goes between LDS-staged banks and (small-LDS kernel) global-ROM
+    ones; 64: mostly between unstaged banks.  Handler counts, IF read-backs and the per-bank sums
+    stay in WRAM 0xC020-0xC04F."""
+    L = ["section 0",
+         "org $0040", "jp h_0", "org $0048", "jp h_1", "org $0050", "jp h_2", "org $0058", "jp h_3", "org $0060", "jp h_4",
+         "org $0100", "nop", "jp start", "org $0150",
+         "start:", "di", "ld sp, $dff0", "ld a, $e3", "ldh [$40], a",
+         "main:",
+         "ld a, [$c030]", "inc a", "ld [$c030], a", "ld b, a",
+         # the timer runs in every other stretch of 8 passes (TAC 5 / 1): with it on, K1 takes its
+         # timer stage — which re-derives the pending bit — every iteration
+         "and $08", "rrca", "or $01", "ldh [$07], a",
+         # the joypad mixes into the masks, so envs differ
+         "ld a, $10", "ldh [$00], a", "ldh a, [$00]", "ldh a, [$00]", "xor b", "ld e, a",
+         "and $1f", "ldh [$ff], a",                       # IE
+         "ld a, e", "rrca", "and $1f", "ldh [$0f], a",    # IF (IME off: nothing dispatches yet)
+         "ldh a, [$0f]", "ld [$c031], a",
+         "ld hl, $ff0f", "set 2, [hl]", "res 0, [hl]",    # read-modify-writes of IF
+         "ldh a, [$0f]", "ld [$c032], a",
+         "ei", "nop", "nop", "di",                        # the pending ones dispatch here
+         "ld a, e", "and $03", "jr nz, .keep", "xor a", "ldh [$0f], a", ".keep:",
+         "ld a, $1f", "ldh [$ff], a", "xor a", "ldh [$ff], a",  # IE on and off again with IF as it is
+         "ld a, 1", "ld [$2000], a", "ld a, e", "and $07", "inc a", "ld c, a", "call $4000",
+         "jp main"]
+    for k in range(5):
+        L += [f"h_{k}:", "push af", f"ld a, [${0xC040 + k:04x}]", "inc a", f"ld [${0xC040 + k:04x}], a", "pop af", "reti"]
+    for k in range(1, n_banks):
+        nxt = (k * 5) % (n_banks - 1) + 1
+        L += [f"section {k}", "org $4000", f"hop_{k}:",
+              "ld hl, $c020", "ld a, [hl]", f"add a, ${(k * 13) & 0xFF:02x}", "ld [hl], a",
+              f"ld a, {nxt}", "ld [$2000], a",            # switch from inside the switchable bank
+              f"ld b, ${(k * 29 + 7) & 0xFF:02x}",        # fetched from bank `nxt`: its own immediate
+              "ld a, [$c021]", "add a, b", "ld [$c021], a",
+              "dec c", f"jr nz, hop_{k}", "ret"]
+    return build_rom("\n".join(L), n_banks=n_banks, title="IRQBANK")
+
+
 def copydata_rom() -> bytes:
     """pokered's CopyData loop (home/copy.asm) and its B/C-swapped twin — which K1 runs in blocks of
     whole passes (pk_step.hip pk_copy_loop) — called with per-env parameters from the joypad and an

@@ -94,8 +94,18 @@ typedef void* hipStream_t;
 typedef void* hipEvent_t;
 enum { hipSuccess = 0, hipErrorInvalidValue = 1, hipErrorOutOfMemory = 2 };
 enum hipMemcpyKind { hipMemcpyHostToDevice, hipMemcpyDeviceToHost, hipMemcpyDeviceToDevice, hipMemcpyHostToHost };
-static inline const char* hipGetErrorString(hipError_t) { return "hostsim error"; }
-static inline hipError_t hipGetLastError() { return hipSuccess; }
+// K1's lane-invariant checks (pk_step.hip pk_check_lane): a failed check is recorded
+// (hostsim_rt.cpp) and reported by the next hipGetLastError — the launch's own error check in
+// pk_launch_step — so the C ABI call that ran the kernel fails with the first failure's text
+enum { hipErrorAssert = 710 };
+extern "C" int pk_sim_check_pending(void);
+extern "C" const char* pk_sim_check_message(void);
+static inline const char* hipGetErrorString(hipError_t e) { return e == hipErrorAssert ? pk_sim_check_message() : "hostsim error"; }
+static inline hipError_t hipGetLastError() { return pk_sim_check_pending() ? (hipError_t)hipErrorAssert : hipSuccess; }
+extern "C" void pk_sim_check_fail(uint32_t env, const char* what);
+#ifndef PK_NO_CHECK
+#define PK_CHECK(env, cond, what) do { if (!(cond)) pk_sim_check_fail(env, what); } while (0)
+#endif
 static inline hipError_t hipSetDevice(int) { return hipSuccess; }
 static inline hipError_t hipDeviceSynchronize() { return hipSuccess; }
 enum hipDeviceAttribute_t { hipDeviceAttributeMultiprocessorCount = 1 };

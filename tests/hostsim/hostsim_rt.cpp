@@ -1,6 +1,9 @@
 // Host-simulation runtime (see hip/hip_runtime.h). TEST INFRASTRUCTURE ONLY.
 #include "hip/hip_runtime.h"
 
+#include <mutex>
+#include <string>
+
 thread_local dim3 threadIdx;
 thread_local dim3 blockIdx;
 dim3 blockDim;
@@ -128,3 +131,21 @@ extern "C" uint64_t pk_sim_iter_get(uint32_t env, uint32_t* out, uint64_t cap) {
     if (out) memcpy(out, g_iter[env].data(), (n < cap ? n : cap) * 4);
     return n;
 }
+
+// ---- K1 lane-invariant failures (PK_CHECK, pk_step.hip pk_check_lane) ----
+static std::mutex g_check_mu;
+static uint64_t g_check_n = 0;
+static std::string g_check_first, g_check_msg;
+extern "C" void pk_sim_check_fail(uint32_t env, const char* what) {
+    std::lock_guard<std::mutex> l(g_check_mu);
+    if (g_check_n++ == 0) g_check_first = "K1 invariant: " + std::string(what) + " (env " + std::to_string(env) + ")";
+}
+// reported (and cleared) once: the first failure's text and the count
+extern "C" int pk_sim_check_pending(void) {
+    std::lock_guard<std::mutex> l(g_check_mu);
+    if (!g_check_n) return 0;
+    g_check_msg = g_check_first + ", " + std::to_string(g_check_n) + " failed checks";
+    g_check_n = 0;
+    return 1;
+}
+extern "C" const char* pk_sim_check_message(void) { return g_check_msg.c_str(); }

@@ -30,6 +30,43 @@ def test_environment_reset_step_shapes(tmp_path):
 
 
 @pytest.mark.gpu
+def test_environment_200_steps_vs_oracle():
+    """configs[0]'s shape (test.py:16-29: one Environment, step(0) repeatedly) on the HIP path, env
+    by env against the oracle emulator + the reward oracle (oracle/reward.py): the reset obs, then
+    for each of 200 step(0) calls the (72,80,4) obs, the float64 reward, done and WRAM C000-DFFF,
+    and the whole v9 machine state at the end."""
+    from oracle import oracle as O
+    from oracle import reward as R
+    from pokegym_amd.env import Environment
+    grey = np.array([0xFF, 0x99, 0x55, 0x00], np.uint8)
+    rom, state = pkbench_power_on()
+    env = Environment(rom_path=rom, state_path=state)
+    gb = O.GB(rom, state)
+
+    class Bus:
+        def r(self, a):
+            return gb.read(a)
+
+        def w(self, a, v):
+            gb.write(a, v & 0xFF)
+
+    st, bus = R.EnvState(), Bus()
+    want = R.reset(st, bus, lambda: grey[gb.screen()], reload=lambda: gb.load_state(state))
+    obs, info = env.reset()
+    assert np.array_equal(obs, want)
+    for t in range(200):
+        obs, rew, term, trunc, info = env.step(0)
+        gb.run_action(0)
+        o, r, d = R.step(st, bus, 0, grey[gb.screen()])
+        assert st.err == 0
+        assert np.array_equal(obs, o), f"step {t + 1}: obs differs"
+        assert rew == r and term == bool(d), (t + 1, rew, r, term, d)
+        assert np.array_equal(env.emu.peek(0, 0xC000, 0x2000), gb.wram().tobytes()), f"step {t + 1}: WRAM differs"
+    assert env.emu.snapshot(0) == gb.save_state()
+    env.close()
+
+
+@pytest.mark.gpu
 def test_vecenv_steps_and_autoresets():
     import torch
     from pokegym_amd.env import VecEnv

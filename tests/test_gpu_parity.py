@@ -99,6 +99,12 @@ def test_game_rom_parity_wave_shapes(lanes, monkeypatch):
 WG512_CASES = [("16", True, -1), ("16", False, 21),
                ("32", True, -1), ("32", True, 0), ("32", False, 3), ("32", False, -1),
                ("64", True, 47), ("64", False, -1)]
+# PK_PARITY_EXTENDED=1: the whole cross product (3 wave widths x rendered/headless x pkbench and four
+# fuzz ROMs, 30 cases) — outside the driver's time-limited suite; one run of it on the final kernel is
+# committed under profiles/ 
+if os.environ.get("PK_PARITY_EXTENDED") == "1":
+    WG512_CASES = [(lanes, render, seed) for lanes in ("16", "32", "64") for render in (True, False)
+                   for seed in (-1, 0, 3, 21, 47)]
 
 
 @pytest.mark.parametrize("lanes,render,seed", WG512_CASES)
@@ -219,6 +225,25 @@ def test_io_edges_parity(n_banks):
     from pokegym_amd.testrom.fuzz import io_edge_rom
     n = 256
     gpu, ref = _run_both(io_edge_rom(n_banks), None, n, 4, 7)
+    bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
+    assert not bad, bad[:4]
+
+
+@pytest.mark.parametrize("n_banks,small", [(8, False), (8, True), (64, False), (64, True)])
+def test_irq_bank_parity(n_banks, small, monkeypatch):
+    """IF / IE writes and read-modify-writes with IME off, then an IME-on window where what they left
+    pending dispatches (K1's cached pending-interrupt bit), the timer on in half of the passes; ROM
+    bank switches issued from code in the switchable bank, the next instruction fetched from the new
+    bank (K1's prefetch across a slow write) — fuzz.py irq_bank_rom; in the default kernel (8 banks:
+    six staged in LDS, 64: the unstaged-bank instance) and in the small-LDS kernel the VecEnv
+    sub-batches run (2 slots: most switches go to or from a global-ROM bank)."""
+    from pokegym_amd.testrom.fuzz import irq_bank_rom
+    if small:
+        monkeypatch.setenv("PK_K1_SMALL", "1")
+        monkeypatch.setenv("PK_WAVE_LANES", "32")
+        monkeypatch.setenv("PK_K1_BLOCK", "256")
+    n = 256
+    gpu, ref = _run_both(irq_bank_rom(n_banks), None, n, 4, 13)
     bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
     assert not bad, bad[:4]
 

@@ -45,7 +45,10 @@ def _check_states(rom, state, actions, emu, futs, headless):
 
 
 def test_config3_geometry_65536_envs():
-    """configs[2]: 65,536 envs, rendered frame 24, random actions — the benchmarked launch."""
+    """configs[2]'s env count, image interleave (32-env waves) and rendered frame 24 as ONE
+    whole-handle launch (pk_step_kernel, 512-thread workgroups, wave priority).  Not the benchmark's
+    own launch: bench.py steps configs[2] through VecEnv sub-batches on the small-LDS kernel, which
+    test_config3_flow_vs_oracle_per_env checks at this size."""
     import torch
     from pokegym_amd.emulator import BatchedEmulator
     from pokegym_amd.testrom.game import game_rom
@@ -249,6 +252,56 @@ def test_config4_flow_vs_oracle_per_env():
         vec.close()
     assert np.array_equal(got_done, want_done), np.argwhere(got_done != want_done)[:5]
     half = n // 2
+    assert want_done[:, :half].sum() == half and want_done[:, half:].sum() == half   # one done per env
+    for k, t in enumerate(check_at):
+        bad = np.nonzero(got_dig[k] != want_dig[k])[0]
+        assert not len(bad), f"after step {t + 1}: {len(bad)}/{n} envs differ, first {bad[:8].tolist()}"
+
+
+def test_config3_flow_vs_oracle_per_env():
+    """The benchmarked configs[2] flow itself (bench.py's default command), env by env: VecEnv with
+    65,536 envs in 2 sub-batches of 32,768 (PufferLib batch_size, README.md:116-118), each stepped by
+    pk_step_range on its own stream — the small-LDS K1 with 32-env waves in 256-thread workgroups, no
+    wave priority, sub-batch 1 at env0 = 32,768 of a 65,536-env image interleave (asserted through
+    pk_launch_shape) — over 6 recv/send env-steps with max_episode_steps 4, so every env auto-resets
+    on the device (pk_reset_range template reload, done = time >= max_episode_steps,
+    environment.py:1612-1613) after its 4th step.  Whole-machine v9 digests of every env after step 3
+    (before any reset) and after step 6 (2 steps into the second episode), and the dones recv()
+    hands back, == the oracle replaying the same actions with reset-on-done."""
+    import torch
+    from pokegym_amd.env import VecEnv
+    from pokegym_amd.testrom.game import game_rom
+    rom, n, steps, max_steps = game_rom(), 65536, 6, 4
+    half = n // 2
+    actions = np.random.default_rng(65538).integers(0, 8, (steps, n), dtype=np.uint8)
+    check_at = (2, steps - 1)
+    with OP.pool() as ex:
+        futs = OP.reset_flows(ex, rom, None, actions, max_steps, check_at, chunk=1024)
+        vec = VecEnv(n, rom=rom, power_on=True, reward=False, max_episode_steps=max_steps, log_interval=0,
+                     batch_size=half)
+        assert vec.num_batches == 2
+        for e0 in (0, half):   # the launch bench.py's configs[2] line times
+            assert vec.emu.launch_shape(e0, half) == {"small": True, "wave_lanes": 32, "block": 256, "prio": False,
+                                                      "all_staged": False}, vec.emu.launch_shape(e0, half)
+        acts = torch.from_numpy(actions).to(vec.device)
+        vec.async_reset()
+        got_done = np.zeros((steps, n), np.uint8)
+        got_dig = []
+        for t in range(steps):
+            for _ in range(vec.num_batches):
+                obs, rew, term, trunc, infos, ids, masks = vec.recv()
+                sl = vec.current_envs()
+                if t > 0:   # the terminals of this sub-batch's step t-1
+                    got_done[t - 1, sl] = term.to(torch.uint8).cpu().numpy()
+                vec.send(acts[t, sl])
+            if t in check_at:
+                vec._join_streams()
+                torch.cuda.synchronize()
+                got_dig.append(gpu_digests(vec.emu))
+        got_done[steps - 1] = vec.emu.terminals.cpu().numpy()
+        want_dig, want_done = OP.gather_reset_flows(futs, len(check_at), steps, n)
+        vec.close()
+    assert np.array_equal(got_done, want_done), np.argwhere(got_done != want_done)[:5]
     assert want_done[:, :half].sum() == half and want_done[:, half:].sum() == half   # one done per env
     for k, t in enumerate(check_at):
         bad = np.nonzero(got_dig[k] != want_dig[k])[0]

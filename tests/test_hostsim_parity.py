@@ -63,6 +63,15 @@ def test_hostsim_io_edges(n_banks):
     assert check(io_edge_rom(n_banks), 8, 3, 7) == []
 
 
+@pytest.mark.parametrize("n_banks", [8, 64])
+def test_hostsim_irq_bank(n_banks):
+    """IF / IE writes (K1's cached pending-interrupt bit) and ROM-bank switches issued from code in
+    the switchable bank (K1's prefetch across a slow write) — pokegym_amd/testrom/fuzz.py
+    irq_bank_rom; the loop-top invariant checks (pk_check_lane) run on every iteration."""
+    from pokegym_amd.testrom.fuzz import irq_bank_rom
+    assert check(irq_bank_rom(n_banks), 8, 3, 13) == []
+
+
 def test_hostsim_frame_watchdog():
     """The frame watchdog: LCD switched off faster than once per frame (its clock restarts, so
     frames end on the budget), joypad-dependent passes, timer stretches with TIMA interrupts
