@@ -23,6 +23,9 @@ test_horizon_64_bank_rom runs the 6-slot kernel's unstaged-bank instance.  PK_HO
 adds the shape no benchmark launches any more (512-thread workgroups of 16-env waves) — not part
 of the driver's suite.
 
+PK_HORIZON_EXTENDED=1 also runs test_horizon_10k_continuous_small_l32: the 64 trajectories as one
+continuous 10,000-step run in the headline's kernel shape, compared every 500 steps.
+
 test_horizon_65536_envs runs configs[2]'s own launch (65,536 envs) continuously for 240 steps and
 compares one env of every workgroup with the oracle."""
 import os
@@ -123,6 +126,36 @@ def test_horizon_10k_segments(horizon, part):
             bad.append((int(step), int(j)))
     assert not bad, f"[{st['shape']}] {len(bad)} (step, trajectory) checkpoints differ: {bad[:8]}"
     st["ok"] = True
+
+
+@pytest.mark.skipif(os.environ.get("PK_HORIZON_EXTENDED") != "1",
+                    reason="~5 min of GPU time: PK_HORIZON_EXTENDED=1 (one recorded run per kernel, profiles/)")
+def test_horizon_10k_continuous_small_l32(oracle_horizon):
+    """The 64 trajectories as ONE continuous 10,000-step device run (no oracle state ever loaded) in
+    the headline's kernel shape — the small-LDS K1 with 32-env waves in 256-thread workgroups, as
+    the VecEnv sub-batches of configs[2] run — the whole v9 state compared with the oracle every 500
+    steps.  (K1 recomputes every lane-cached value — the pending-interrupt bit, the tick limit, the
+    prefetch, the HRAM code mirror, the ROM-bank slot — from the stored state at the entry of every
+    launch, i.e. every env-step, so the segmented form above sees the same kernel entries; this run
+    also rules out drift in anything carried across launches.)"""
+    import torch
+    from pokegym_amd.emulator import BatchedEmulator
+    rom, actions, dig, _ = oracle_horizon
+    emu = _with_shape("small_l32", lambda: BatchedEmulator(rom, NTRAJ, render=True))
+    assert emu.launch_shape()["small"] and emu.launch_shape()["wave_lanes"] == 32
+    acts = torch.from_numpy(np.ascontiguousarray(actions)).to(emu.device)
+    bad = []
+    for t in range(TOTAL):
+        emu.step(acts[t])
+        if (t + 1) % 500 == 0:
+            torch.cuda.synchronize()
+            got = oracle.state_digests(emu.snapshot_range(0, NTRAJ))
+            bad += [(t + 1, int(j)) for j in np.nonzero(got != dig[(t + 1) // EVERY - 1])[0]]
+            print(f"continuous small_l32: step {t + 1}, {len(bad)} differing checkpoints so far", flush=True)
+            if bad:
+                break
+    emu.close()
+    assert not bad, f"{len(bad)} (step, trajectory) checkpoints differ: {bad[:8]}"
 
 
 def test_horizon_65536_envs():

@@ -6,7 +6,8 @@ counted) and reports, per guest region and per env-step: accesses, the distinct 
 the lane-interleaved image an env touches (W envs per interleave: a line holds 128 / W guest bytes
 of W envs), and per wave iteration the lines a wave's lanes touch together (what one load or store
 instruction of the wave costs the memory pipe).
-usage: python tools/mem_stats.py [wave_lanes=16] [steps=4] [n=256] [--warp]"""
+usage: python tools/mem_stats.py [wave_lanes=16] [steps=4] [n=256] [--warp] [--writes]
+(--writes: stores only, as bounds on the L2's write-back bytes per env-step)"""
 import ctypes
 import os
 import sys
@@ -98,6 +99,39 @@ def main():
             for r, _, _ in s:
                 wave_lines[r] += 1
     es = n * steps
+    if "--writes" in sys.argv:
+        # stores only: per region, the env-step's distinct 128-byte lines written (each written back
+        # once per step at best: the lower bound of the L2's write-backs) and the wave-level store
+        # line touches (each written back on its own: the upper bound when a dirty line is evicted
+        # between two stores to it), both in bytes per env-step of the 32-byte sectors written
+        wl_lines, wl_env = Counter(), Counter()
+        for w0 in range(0, n, wl):
+            by_it = defaultdict(set)
+            envlines = defaultdict(set)
+            for e in range(w0, min(n, w0 + wl)):
+                b = recs[e]
+                b = b[((b >> 16) & 1) == 1]
+                for i, p in zip((b >> 20).astype(np.int64).tolist(), (b & 0xFFFF).astype(np.int64).tolist()):
+                    by_it[i].add((region(p), p // per_line))
+                    envlines[region(p)].add(p // per_line)
+            for st in by_it.values():
+                for r, _ in st:
+                    wl_lines[r] += 1
+            for r, st in envlines.items():
+                wl_env[r] += len(st)
+        print(f"stores, wave_lanes {wl}, {n} envs x {steps} env-steps: bytes per env-step if each written line is "
+              f"written back once per step (lower) / once per wave-iteration store (upper), 32-byte sectors of "
+              f"{wl} envs x {per_line} guest bytes")
+        print(f"{'region':30s} {'stores/es':>9s} {'lines/step/wave':>16s} {'lower B/es':>11s} {'upper B/es':>11s}")
+        lo_t = up_t = 0.0
+        for r in sorted(wl_lines, key=lambda r: -wl_lines[r]):
+            lo = wl_env[r] * 128 / steps / n            # whole lines, once per step, per env
+            up = wl_lines[r] * 32 / steps / n           # one 32-byte sector per line a wave's store touches
+            lo_t += lo
+            up_t += up
+            print(f"{r:30s} {acc[(r, 1)] / es:9.1f} {wl_env[r] / steps / (n // wl):16.1f} {lo:11.1f} {up:11.1f}")
+        print(f"{'total':30s} {'':9s} {'':16s} {lo_t:11.1f} {up_t:11.1f}")
+        return
     tot_acc = sum(acc.values())
     print(f"wave_lanes {wl}, {n} envs x {steps} env-steps{' (door-warp state)' if warp else ''}: "
           f"{tot_acc / es:.0f} fast-path image accesses per env-step; wave iterations with an access: "
