@@ -536,7 +536,11 @@ def main():
                 "traffic_per_env_step": (stamp or {}).get("hbm_bytes_per_env_step_k1"),
                 "traffic_source": (f"{stamp_src}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this "
                                    "workload (K1 only; L2 memory-side requests, Infinity-Cache hits included; "
-                                   "not measured inside this run)") if stamp else None,
+                                   "not measured inside this run); counted at "
+                                   + ("the timed steps' occupancy (two waves per SIMD: pmc_stamp.regime)"
+                                      if stamp.get("regime") else "one launch alone")) if stamp else None,
+                "traffic_serialised_per_env_step": ((stamp or {}).get("serialised_record") or {}).get(
+                    "hbm_bytes_per_env_step_k1"),
                 "bytes_per_env_step": B,
                 "span_ms": round(span_s * 1e3, 3),
                 "k1_ms": round(k1_s * 1e3, 3),
@@ -548,7 +552,7 @@ def main():
         }
         if stamp:
             out["pmc_stamp"] = {k: stamp[k] for k in ("valu_busy_pct", "valu_utilization_pct", "wait_any_pct",
-                                                      "waves_per_simd", "source") if k in stamp}
+                                                      "waves_per_launch", "regime", "source") if k in stamp}
             if "issue" in stamp:
                 out["roofline"]["issue"] = stamp["issue"]
         out["collectives"] = {

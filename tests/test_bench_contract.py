@@ -36,6 +36,13 @@ def test_pmc_stamp_fields_and_source(w):
     assert stats, d["source"]
     for f in files:
         assert os.path.exists(os.path.join(HERE, f)), f
+    # the VecEnv workloads (two concurrent sub-batch launches) are counted at the timed steps'
+    # occupancy, two waves per SIMD (2,048 waves on 1,024 SIMDs), and say so; the serialised
+    # one-launch record sits beside it
+    if w != "config2":
+        assert "two waves per SIMD" in d.get("regime", ""), w
+        assert d["waves_per_launch"] == 2048 and "serialised_record" in d
+        assert d["serialised_record"]["waves_per_launch"] == 1024
     rows = list(csv.DictReader(open(os.path.join(HERE, stats[0]))))
     k1 = [r for r in rows if "pk_step_kernel" in r["Name"]]
     assert k1, stats[0]

@@ -9,7 +9,8 @@
 #         workgroups per CU = two 32-env waves per SIMD) as ONE launch: the whole 65,536-env handle
 #         through the small-LDS kernel (PK_K1_SMALL=1, VecEnv with one batch) — rocprofv3 --pmc
 #         serialises dispatches, so the bench's two concurrent sub-batch launches are profiled one
-#         at a time (one wave per SIMD) in the prof session
+#         at a time (one wave per SIMD) in the prof session; likewise configs[3]/[4]'s shards
+#         (config4/config5: 32,768 envs in 16-env waves, two per SIMD)
 #   stamp phase stamps (-DPK_STAMP build, whole-handle launches; config3small = the small-LDS
 #         kernel the VecEnv sub-batches run, at their two-waves-per-SIMD occupancy)
 # Each GPU step has its own time limit; the chain stops at the first failure.
@@ -28,7 +29,8 @@ if [ "$1" = prof ]; then
 elif [ "$1" = prof2 ]; then
   bash $R/tools/gpu_round_prof.sh ${TAG}b "config2|--workload config2" "config3_b64|--workload config3 --rom-banks 64"
 elif [ "$1" = conc ]; then
-  PK_K1_SMALL=1 bash $R/tools/gpu_round_prof.sh ${TAG}c "config3_2wps|--workload config3 --batches 1"
+  PK_K1_SMALL=1 bash $R/tools/gpu_round_prof.sh ${TAG}c "config3_2wps|--workload config3 --batches 1" \
+      "config4_2wps|--workload config4 --batches 1" "config5_2wps|--workload config5 --batches 1"
 elif [ "$1" = stamp ]; then
   cd $R && bash tools/gpu_stamp.sh $TAG "config3small|PK_K1_SMALL=1 --workload config3" "config3|--workload config3" \
       "config4|--workload config4" "config2|--workload config2"
