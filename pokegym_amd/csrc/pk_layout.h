@@ -87,7 +87,7 @@ enum {
     PK_R_MISC,       // joypad directional | standard<<8 | (ly_window+1)<<16 (u8)
     PK_R_TIME,       // env-steps since reset (pokegym `self.time`, environment.py:1338)
     PK_R_ICOUNT,     // emulated instructions in the last pk_step (perf counter)
-    PK_R_RFLAGS,     // render bookkeeping of the last step: blank<<0 | pending-lines<<8
+    PK_R_RFLAGS,     // render bookkeeping of the last step: blank<<0 | (lines left for K2)<<8
     PK_NREGS
 };
 

@@ -140,10 +140,19 @@ __device__ inline void render_line(const Mem& m, u32 y, u32 lat0, u32 lat1, int 
     }
 }
 
-// rasterise every latched-but-pending line of this lane now (before VRAM/OAM change).  Rare
-// path: kept out of line with by-value arguments so the step loop's state stays in VGPRs.
+// The pending-lines word K1 keeps per lane (St.npend): 0 = no latched line waits for rasterisation,
+// else (highest pending line + 1) | lowest pending line << 16 — lines are latched at mode-0 events
+// (and in bulk by the HALT skip-ahead), so flush_lines reads only that range's latch flags
+__device__ __forceinline__ u32 pend_add(u32 p, u32 lo, u32 hi) {
+    const u32 h1 = hi + 1u;
+    return p == 0u ? (h1 | (lo << 16)) : ((((p & 0xFFFFu) > h1) ? (p & 0xFFFFu) : h1) | (((p >> 16) < lo ? (p >> 16) : lo) << 16));
+}
+
+// rasterise every latched-but-pending line of this lane now (before VRAM/OAM change); pend = the
+// lane's pending-lines word (pend_add).  Rare path: kept out of line with by-value arguments so
+// the step loop's state stays in VGPRs.
 __device__ __noinline__ static void flush_lines(u32* lat, u32 lat_stride, u8* screen, u8* gbase, u32 il, u32 sh, u32 lane,
-                                                u32 env, u32 gid) {
+                                                u32 env, u32 gid, u32 pend) {
     Mem m;
     m.g = gbase;
     m.lane = il;
@@ -151,13 +160,21 @@ __device__ __noinline__ static void flush_lines(u32* lat, u32 lat_stride, u8* sc
     u32* lat0 = lat;
     u32* lat1 = lat + lat_stride;
     u32* lat2 = lat + 2u * lat_stride;
-    // the latch flags are read 16 lines at a time (independent loads: one memory round trip per
-    // batch instead of one per line)
-    for (u32 y0 = 0; y0 < PK_ROWS; y0 += 16u) {
+#ifndef PK_FLUSH_FULL
+    const u32 ylo = pend >> 16, yend = pend & 0xFFFFu;   // lines [ylo, yend)
+#else
+    const u32 ylo = 0u, yend = pend ? PK_ROWS : 0u;       // (A/B diagnostic: every line's flag)
+#endif
+    // the latch flags of the range are read 16 lines at a time (independent loads: one memory
+    // round trip per batch instead of one per line)
+    for (u32 y0 = ylo; y0 < yend; y0 += 16u) {
         u32 f[16];
 #pragma unroll
-        for (u32 k = 0; k < 16u; k++) f[k] = lat2[(gid * PK_ROWS + y0 + k) * PK_LANES + lane];
         for (u32 k = 0; k < 16u; k++) {
+            const u32 y = y0 + k < PK_ROWS ? y0 + k : PK_ROWS - 1u;   // (reads past the range: never used)
+            f[k] = lat2[(gid * PK_ROWS + y) * PK_LANES + lane];
+        }
+        for (u32 k = 0; k < 16u && y0 + k < yend; k++) {
             const u32 y = y0 + k, idx = (gid * PK_ROWS + y) * PK_LANES + lane, l2 = f[k];
             if (l2 & 0x100u) {
                 render_line(m, y, lat0[idx], lat1[idx], (int)(l2 & 0xFFu) - 1, screen + (size_t)env * PK_SCREEN + y * PK_COLS);

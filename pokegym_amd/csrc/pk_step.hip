@@ -196,7 +196,7 @@ struct St {
     u32 rlim;             // ROM addresses below it are staged: 0x8000, or 0x4000 when the bank is not
     u32 lim;              // tick_lim(): clock below it = no LCD event, no LCD-off frame end, timer off,
                           // no frame watchdog
-    u32 npend;            // latched, not yet rasterised lines
+    u32 npend;            // latched, not yet rasterised lines: 0 = none, else the range (pk_render.h pend_add)
     u32 render, blank, frame_done;
 };
 
@@ -426,7 +426,7 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
                 break;
             case 0xFF46: {  // OAM DMA: instantaneous 160-byte copy (pyboy mb.transfer_DMA)
                 if (s.npend) {
-                    flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.sh, c.glane, c.env, c.gid);
+                    flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.sh, c.glane, c.env, c.gid, s.npend);
                     s.npend = 0;
                 }
                 const u32 src = v << 8;
@@ -462,7 +462,7 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
         return;
     }
     if (s.npend && vram_or_oam(a)) {
-        flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.sh, c.glane, c.env, c.gid);
+        flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.sh, c.glane, c.env, c.gid, s.npend);
         s.npend = 0;
     }
     st_img(c, fast_phys(a), v);
@@ -814,7 +814,7 @@ __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc&
     if constexpr (BF) {
         if (PK_RARE(x.wram & (s.npend != 0u))) {
             if (vram_or_oam(x.addr0) | (x.wr2 & vram_or_oam(x.addr1))) {
-                flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.sh, c.glane, env, c.gid);
+                flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.sh, c.glane, env, c.gid, s.npend);
                 s.npend = 0;
                 ev |= PK_EV_FLUSH;
             }
@@ -840,7 +840,7 @@ __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc&
             PK_STAMP_AT(2);
             if (vram_or_oam(x.addr0) | (x.wr2 & vram_or_oam(x.addr1))) {
                 PK_STAMP_AT(11);
-                flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.sh, c.glane, env, c.gid);
+                flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.sh, c.glane, env, c.gid, s.npend);
                 PK_STAMP_AT(10);
                 s.npend = 0;
                 ev |= PK_EV_FLUSH;
@@ -1337,7 +1337,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
                             A.lat[2u * A.lat_stride + idx] = (u32)(lw + 1) | 0x100u;
                         }
                         s.misc = setb8(s.misc, 16, 0u);              // reset after line 143
-                        s.npend += PK_ROWS - y0;
+                        s.npend = pend_add(s.npend, y0, PK_ROWS - 1u);
                     }
                     const u32 skipped = tnew - s.clock;
                     s.divacc += skipped;
@@ -1418,7 +1418,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
                     A.lat[2u * A.lat_stride + idx] = (u32)(lw + 1) | 0x100u;
                     if (ly == PK_ROWS - 1u) lw = -1;
                     s.misc = setb8(s.misc, 16, (u32)(lw + 1));
-                    s.npend += 1u;
+                    s.npend = pend_add(s.npend, ly, ly);
                 }
             }
             if (PK_RARE(!(lcdc & 0x80u) && s.clock >= FRAME_CYCLES)) {  // LCD off: the frame ends on the clock alone
@@ -1487,7 +1487,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
     R[PK_R_MISC * np + env] = s.misc;
     R[PK_R_TIME * np + env] += 1u;
     R[PK_R_ICOUNT * np + env] = icount;
-    R[PK_R_RFLAGS * np + env] = s.blank | (s.npend << 8);
+    R[PK_R_RFLAGS * np + env] = s.blank | sel(s.npend != 0u, 0x100u, 0u);   // bit 8: lines left for K2
 }
 
 hipError_t PK_K1_LAUNCH(const PkStepArgs& a, hipStream_t s) {
