@@ -140,6 +140,11 @@ __device__ inline void render_line(const Mem& m, u32 y, u32 lat0, u32 lat1, int 
     }
 }
 
+// host-simulation hooks (design statistics): a flush_lines call (0) and a line it rasterises (1)
+#ifndef PK_FLUSH_STAT
+#define PK_FLUSH_STAT(rendered) ((void)0)
+#endif
+
 // The pending-lines word K1 keeps per lane (St.npend): 0 = no latched line waits for rasterisation,
 // else (highest pending line + 1) | lowest pending line << 16 — lines are latched at mode-0 events
 // (and in bulk by the HALT skip-ahead), so flush_lines reads only that range's latch flags
@@ -179,7 +184,9 @@ __device__ __noinline__ static void flush_lines(u32* lat, u32 lat_stride, u8* sc
             if (l2 & 0x100u) {
                 render_line(m, y, lat0[idx], lat1[idx], (int)(l2 & 0xFFu) - 1, screen + (size_t)env * PK_SCREEN + y * PK_COLS);
                 lat2[idx] = l2 & ~0x100u;
+                PK_FLUSH_STAT(1);
             }
         }
     }
+    PK_FLUSH_STAT(0);
 }

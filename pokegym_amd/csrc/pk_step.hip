@@ -197,6 +197,7 @@ struct St {
     u32 lim;              // tick_lim(): clock below it = no LCD event, no LCD-off frame end, timer off,
                           // no frame watchdog
     u32 npend;            // latched, not yet rasterised lines: 0 = none, else the range (pk_render.h pend_add)
+    u32 prow;             // tile-map rows those lines read, either map: bit r = row r (pend_hit)
     u32 render, blank, frame_done;
 };
 
@@ -231,6 +232,16 @@ __device__ __forceinline__ u32 fast_phys(u32 a) {
     return sel(a >= 0xFE00u, PK_P_OAM + (a & 0x1FFu), p);
 }
 __device__ __forceinline__ bool vram_or_oam(u32 a) { return (a >= 0x8000u && a < 0xA000u) || (a >= 0xFE00u && a < 0xFEA0u); }
+// Would a write at a change a pending (latched, not yet rasterised) line?  A pending line reads the
+// tile data, the OAM and at most two tile-map rows — its BG row (y + SCY) / 8 and its window row
+// lw / 8, recorded in St.prow at its latch (the bulk latch of the HALT skip-ahead sets every bit).
+// A map write to a row no pending line reads leaves every pending line's pixels as they were at its
+// latch, so the lines stay pending (K2 or a later flush rasterises them from the same bytes); tile
+// data and OAM writes always flush.  pkbench's rendered frames write map rows the pending lines do
+// not show ~12 times per env-step (host simulation), each a flush before
+__device__ __forceinline__ bool pend_hit(u32 prow, u32 a) {
+    return (a - 0x8000u < 0x1800u) | (a - 0xFE00u < 0xA0u) | ((a - 0x9800u < 0x800u) & (((prow >> ((a >> 5) & 31u)) & 1u) != 0u));
+}
 // ROM address staged in LDS?  and its LDS byte index
 __device__ __forceinline__ bool rom_staged(const St& s, u32 a) { return a < s.rlim; }
 __device__ __forceinline__ u32 rom_lds_index(const St& s, u32 a) { return a + sel(a < 0x4000u, 0u, s.rb); }
@@ -428,6 +439,7 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
                 if (s.npend) {
                     flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.sh, c.glane, c.env, c.gid, s.npend);
                     s.npend = 0;
+                    s.prow = 0;
                 }
                 const u32 src = v << 8;
                 if (fast_ram(src) && src < 0xFE00u) {
@@ -461,9 +473,10 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
         }
         return;
     }
-    if (s.npend && vram_or_oam(a)) {
+    if (s.npend && pend_hit(s.prow, a)) {
         flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.sh, c.glane, c.env, c.gid, s.npend);
         s.npend = 0;
+        s.prow = 0;
     }
     st_img(c, fast_phys(a), v);
     hcode_st(c, a, v);
@@ -813,9 +826,10 @@ __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc&
     const PkStepArgs& A = *c.A;
     if constexpr (BF) {
         if (PK_RARE(x.wram & (s.npend != 0u))) {
-            if (vram_or_oam(x.addr0) | (x.wr2 & vram_or_oam(x.addr1))) {
+            if (pend_hit(s.prow, x.addr0) | (x.wr2 & pend_hit(s.prow, x.addr1))) {
                 flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.sh, c.glane, env, c.gid, s.npend);
                 s.npend = 0;
+                s.prow = 0;
                 ev |= PK_EV_FLUSH;
             }
             PK_VM_DRAIN();
@@ -838,11 +852,12 @@ __device__ __forceinline__ void pk_write(St& s, const Ctx& c, u32 env, const Mc&
         // (lines are pending only in the rendered frame: test that first, alone)
         if (PK_RARE(s.npend != 0u)) {
             PK_STAMP_AT(2);
-            if (vram_or_oam(x.addr0) | (x.wr2 & vram_or_oam(x.addr1))) {
+            if (pend_hit(s.prow, x.addr0) | (x.wr2 & pend_hit(s.prow, x.addr1))) {
                 PK_STAMP_AT(11);
                 flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.sh, c.glane, env, c.gid, s.npend);
                 PK_STAMP_AT(10);
                 s.npend = 0;
+                s.prow = 0;
                 ev |= PK_EV_FLUSH;
             }
         }
@@ -1010,6 +1025,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
     s.misc = R[PK_R_MISC * np + env];
     set_rom_bank(s, slot_base((s.mbc & 0xFFu) & A.rom_bank_mask));
     s.npend = 0;
+    s.prow = 0;
     s.blank = 0;
     s.frame_done = 0;
     u32 icount = 0;
@@ -1338,6 +1354,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
                         }
                         s.misc = setb8(s.misc, 16, 0u);              // reset after line 143
                         s.npend = pend_add(s.npend, y0, PK_ROWS - 1u);
+                        s.prow = ~0u;                                 // (their rows: not worth computing here)
                     }
                     const u32 skipped = tnew - s.clock;
                     s.divacc += skipped;
@@ -1411,7 +1428,8 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
                 if (PK_RARE(lcdev && s.render && (s.lcd0 & 0x300u) == 0u && ly < PK_ROWS)) {
                     const u32 wy = bfe8(s.lcd1, 16), wx = bfe8(s.lcd1, 24);
                     int lw = (int)bfe8(s.misc, 16) - 1;
-                    if ((lcdc & 0x20u) && wy <= ly && (int)wx - 7 < (int)PK_COLS) lw += 1;
+                    const bool wl = (lcdc & 0x20u) && wy <= ly && (int)wx - 7 < (int)PK_COLS;
+                    if (wl) lw += 1;
                     const u32 idx = (c.gid * PK_ROWS + ly) * PK_LANES + c.glane;
                     A.lat[idx] = lcdc | (bfe8(s.lcd1, 8) << 8) | (bfe8(s.lcd1, 0) << 16) | (wx << 24);
                     A.lat[A.lat_stride + idx] = wy | ((s.lcd2 & 0xFFFFFFu) << 8);
@@ -1419,6 +1437,9 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
                     if (ly == PK_ROWS - 1u) lw = -1;
                     s.misc = setb8(s.misc, 16, (u32)(lw + 1));
                     s.npend = pend_add(s.npend, ly, ly);
+                    // the map rows this line reads: its BG row, and its window row when the window shows
+                    s.prow |= sel(lcdc & 0x01u, 1u << (((ly + bfe8(s.lcd1, 0)) >> 3) & 31u), 0u)
+                            | sel(wl, 1u << (((u32)lw >> 3) & 31u), 0u);
                 }
             }
             if (PK_RARE(!(lcdc & 0x80u) && s.clock >= FRAME_CYCLES)) {  // LCD off: the frame ends on the clock alone

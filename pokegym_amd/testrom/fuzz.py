@@ -344,6 +344,68 @@ def irq_bank_rom(n_banks: int = 8) -> bytes:
     return build_rom("\n".join(L), n_banks=n_banks, title="IRQBANK")
 
 
+def vram_midframe_rom() -> bytes:
+    """VRAM and OAM writes in the middle of the visible frame — what K1's deferred rasteriser must
+    get right: a line is latched at its mode-0 event and rasterised later (K2 at the step's end, or
+    flush_lines before a write that would change it: pk_step.hip pend_hit).  Each pass waits (LY
+    poll) for a joypad- and pass-dependent line T, then writes one of: a BG-map byte in the row the
+    line just above T shows (pending: must flush) or in a row further down (not yet latched: no
+    flush; about ten writes a frame), a window-map byte in the window's current row or another, a tile-data byte of a tile the
+    maps use, an OAM byte of a visible sprite, SCY (later lines show other rows), LCDC's BG-map
+    select (the other map's rows), or a BG-map byte of the map not shown; BG, window (WY 72, WX 47)
+    and ten 8x8 sprites are on, so every kind of read a line makes is covered."""
+    L = ["wPass equ $c0f0", "wT equ $c0f1",
+         "section 0", "org $0040", "reti", "org $0048", "reti", "org $0050", "reti", "org $0058", "reti", "org $0060", "reti",
+         "org $0100", "nop", "jp start", "org $0150",
+         "start:", "di", "ld sp, $dff0", "xor a", "ldh [$40], a",
+         # tiles 0-15: byte k of tile t = t * 17 ^ k * 29; BG map 9800: (row * 3 + col) & 15; map 9C00: (row + 5 * col) & 15
+         "ld hl, $8000", "ld b, 0", ".t:", "ld a, b", "swap a", "add a, b", "ld c, a", "ld a, l", "and $0f", "ld e, a",
+         "add a, a", "add a, e", "ld e, a", "add a, a", "add a, a", "add a, a", "add a, e", "sub e", "xor c", "ld [hl+], a",
+         "ld a, l", "and $0f", "jr nz, .t", "inc b", "ld a, b", "cp 16", "jr nz, .t",
+         "ld hl, $9800", ".m:", "ld a, h", "sub $98", "ld d, a", "ld a, l", "and $1f", "ld e, a",
+         "ld a, l", "swap a", "rrca", "and $07", "ld c, a", "ld a, d", "add a, a", "add a, a", "add a, a", "add a, c",
+         "ld c, a", "add a, a", "add a, c", "add a, e", "and $0f", "ld [hl+], a", "ld a, h", "cp $9c", "jr nz, .m",
+         ".w9c:", "ld a, l", "and $1f", "ld e, a", "add a, a", "add a, a", "add a, e", "ld e, a", "ld a, l", "swap a",
+         "rrca", "and $07", "add a, e", "add a, h", "and $0f", "ld [hl+], a", "ld a, h", "cp $a0", "jr nz, .w9c",
+         # OAM: sprite n at y = 16 + 13 n, x = 8 + 15 n, tile n, attribute 0 / $20 / $80 by n
+         "ld hl, $fe00", "ld b, 0", ".o:", "ld a, b", "add a, a", "add a, a", "add a, a", "add a, b", "add a, b",
+         "add a, b", "add a, b", "add a, b", "add a, 16", "ld [hl+], a", "ld a, b", "swap a", "sub b", "add a, 8",
+         "ld [hl+], a", "ld a, b", "ld [hl+], a", "ld a, b", "and $03", "rrca", "rrca", "rrca", "ld [hl+], a",
+         "inc b", "ld a, b", "cp 10", "jr nz, .o",
+         ".oz:", "xor a", "ld [hl+], a", "ld a, l", "cp $a0", "jr nz, .oz",
+         "ld a, 72", "ldh [$4a], a", "ld a, 47", "ldh [$4b], a", "ld a, $e4", "ldh [$47], a", "ld a, $d2", "ldh [$48], a",
+         "ld a, $f3", "ldh [$40], a",                         # LCD on, window map 9C00, tile data 8000, BG map 9800
+         "main:",
+         "ld a, $10", "ldh [$00], a", "ldh a, [$00]", "ldh a, [$00]", "and $0f", "ld e, a",
+         "ld a, [wPass]", "inc a", "ld [wPass], a", "ld b, a",
+         # the next line: 5..20 lines after the last one (about ten writes a frame), wrapping below 140
+         "ld a, e", "and $07", "add a, a", "add a, 5", "ld d, a", "ld a, [wT]", "add a, d", "cp 140", "jr c, .tok",
+         "sub 131", ".tok:", "ld [wT], a", "ld d, a",
+         ".ly:", "ldh a, [$44]", "cp d", "jr nz, .ly",
+         # the row (T + SCY) / 8 of the line at T
+         "ldh a, [$42]", "add a, d", "srl a", "srl a", "srl a", "ld c, a",
+         "ld a, b", "and $07", "jr z, .k0", "dec a", "jr z, .k1", "dec a", "jr z, .k2", "dec a", "jr z, .k3",
+         "dec a", "jr z, .k4", "dec a", "jr z, .k5", "dec a", "jr z, .k6", "jp .k7",
+         ".k0:", "ld a, c", "dec a", "jr .bgrow",                     # the row the line above shows: pending
+         ".k1:", "ld a, c", "add a, 3",                               # a row further down: not latched yet
+         ".bgrow:", "and $1f", "ld l, a", "ld h, 0", "add hl, hl", "add hl, hl", "add hl, hl", "add hl, hl", "add hl, hl",
+         "ld a, b", "and $1f", "add a, l", "ld l, a", "ld a, h", "add a, $98", "ld h, a", "ld a, b", "and $0f", "ld [hl], a",
+         "jp main",
+         ".k2:", "ld a, d", "sub 72", "jr c, .k2b", "srl a", "srl a", "srl a", "jr .wrow",   # the window's current row
+         ".k2b:", "ld a, b", "and $07",
+         ".wrow:", "ld l, a", "ld h, 0", "add hl, hl", "add hl, hl", "add hl, hl", "add hl, hl", "add hl, hl",
+         "ld a, b", "and $07", "add a, l", "ld l, a", "ld a, h", "add a, $9c", "ld h, a", "ld a, b", "and $0f", "ld [hl], a",
+         "jp main",
+         ".k3:", "ld a, b", "and $0f", "swap a", "ld l, a", "ld h, $80", "ld a, e", "xor b", "ld [hl], a", "jp main",  # tile data
+         ".k4:", "ld a, b", "rrca", "rrca", "rrca", "and $07", "add a, a", "add a, a", "ld l, a", "ld h, $fe",  # OAM y / x
+         "ld a, b", "rlca", "rlca", "and $01", "add a, l", "ld l, a", "ld a, [hl]", "xor $05", "ld [hl], a", "jp main",
+         ".k5:", "ld a, b", "and $0f", "ldh [$42], a", "jp main",                                   # SCY
+         ".k6:", "ldh a, [$40]", "xor $08", "ldh [$40], a", "jp main",                              # BG map select
+         ".k7:", "ld a, c", "and $1f", "ld l, a", "ld h, 0", "add hl, hl", "add hl, hl", "add hl, hl", "add hl, hl",
+         "add hl, hl", "ld a, h", "add a, $9c", "ld h, a", "ld a, b", "and $0f", "ld [hl], a", "jp main"]   # the other map
+    return build_rom("\n".join(L), n_banks=2, title="VRAMMID")
+
+
 def copydata_rom() -> bytes:
     """pokered's CopyData loop (home/copy.asm) and its B/C-swapped twin — which K1 runs in blocks of
     whole passes (pk_step.hip pk_copy_loop) — called with per-env parameters from the joypad and an

@@ -142,6 +142,9 @@ extern "C" void pk_sim_iter(uint32_t env, uint32_t ev);
 // per-iteration microcode index (design statistics: opcode uniformity of a wave)
 extern "C" void pk_sim_iter_op(uint32_t env, uint32_t di);
 #define PK_ITER_OP(env, di) pk_sim_iter_op(env, di)
+// flush_lines calls (0) and the lines they rasterise (1) (design statistics)
+extern "C" void pk_sim_flush_stat(uint32_t rendered);
+#define PK_FLUSH_STAT(rendered) pk_sim_flush_stat(rendered)
 // fast-path RAM-image accesses (tools/mem_stats.py)
 extern "C" void pk_sim_memref(uint32_t env, uint32_t kind, uint32_t phys);
 #define PK_MEMREF(env, kind, phys) pk_sim_memref(env, kind, phys)

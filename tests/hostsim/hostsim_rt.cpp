@@ -1,6 +1,7 @@
 // Host-simulation runtime (see hip/hip_runtime.h). TEST INFRASTRUCTURE ONLY.
 #include "hip/hip_runtime.h"
 
+#include <atomic>
 #include <mutex>
 #include <string>
 
@@ -57,6 +58,7 @@ void pk_sim_launch(const char* name, dim3 grid, dim3 block, const std::function<
     for (auto& th : ts) th.join();
 }
 
+#include <atomic>
 #include <mutex>
 static std::vector<uint32_t> g_trace;
 static uint32_t g_trace_env = 0xFFFFFFFFu;
@@ -149,3 +151,8 @@ extern "C" int pk_sim_check_pending(void) {
     return 1;
 }
 extern "C" const char* pk_sim_check_message(void) { return g_check_msg.c_str(); }
+
+// ---- flush_lines statistics (PK_FLUSH_STAT): calls, lines rasterised ----
+static std::atomic<uint64_t> g_flush_calls{0}, g_flush_lines{0};
+extern "C" void pk_sim_flush_stat(uint32_t rendered) { (rendered ? g_flush_lines : g_flush_calls)++; }
+extern "C" void pk_sim_flush_get(uint64_t* out) { out[0] = g_flush_calls.exchange(0); out[1] = g_flush_lines.exchange(0); }

@@ -248,6 +248,37 @@ def test_irq_bank_parity(n_banks, small, monkeypatch):
     assert not bad, bad[:4]
 
 
+@pytest.mark.parametrize("small", [False, True])
+def test_vram_midframe_parity(small, monkeypatch):
+    """VRAM / OAM / SCY / LCDC writes in the middle of the visible frame, about ten a frame, at map rows
+    the pending (latched, not yet rasterised) lines show and rows they do not, tile data, OAM, the
+    window's rows and the map not shown (fuzz.py vram_midframe_rom): K1 rasterises pending lines
+    before a write only when the write would change one of them (pk_step.hip pend_hit); whole state
+    and screen vs the oracle, in the default kernel and in the small-LDS kernel of the VecEnv
+    sub-batches."""
+    from pokegym_amd.testrom.fuzz import vram_midframe_rom
+    if small:
+        monkeypatch.setenv("PK_K1_SMALL", "1")
+        monkeypatch.setenv("PK_WAVE_LANES", "32")
+        monkeypatch.setenv("PK_K1_BLOCK", "256")
+    import torch
+    from pokegym_amd.emulator import BatchedEmulator
+    rom, n, steps = vram_midframe_rom(), 256, 6
+    actions = np.random.default_rng(17).integers(0, 9, size=(steps, n), dtype=np.uint8)
+    emu = BatchedEmulator(rom, n, render=True)
+    for t in range(steps):
+        emu.step(torch.from_numpy(actions[t]).to(emu.device))
+    torch.cuda.synchronize()
+    gpu = [emu.snapshot(e) for e in range(n)]
+    scr = emu.screen.cpu().numpy()
+    emu.close()
+    ref, ref_scr = oracle.batch_run(rom, None, actions)
+    grey = np.array([0xFF, 0x99, 0x55, 0x00], np.uint8)
+    bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
+    assert not bad, bad[:4]
+    assert all(np.array_equal(scr[e], grey[ref_scr[e]]) for e in range(n))
+
+
 def warp_actions(n, seed=5):
     """Actions (6, n) from the warp fixture's state: columns 0..n/2-1 the recorded actions (they
     walk through a door at step 2: pkbench's map load with the LCD off for ~5 frames), the rest

@@ -72,6 +72,14 @@ def test_hostsim_irq_bank(n_banks):
     assert check(irq_bank_rom(n_banks), 8, 3, 13) == []
 
 
+def test_hostsim_vram_midframe():
+    """VRAM / OAM / SCY / LCDC writes in the middle of the visible frame, at rows the pending (latched,
+    not yet rasterised) lines show and rows they do not (fuzz.py vram_midframe_rom): K1 flushes only
+    before writes that would change a pending line (pk_step.hip pend_hit); screens vs the oracle."""
+    from pokegym_amd.testrom.fuzz import vram_midframe_rom
+    assert check(vram_midframe_rom(), 32, 6, 17) == []
+
+
 def test_hostsim_frame_watchdog():
     """The frame watchdog: LCD switched off faster than once per frame (its clock restarts, so
     frames end on the budget), joypad-dependent passes, timer stretches with TIMA interrupts

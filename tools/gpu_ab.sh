@@ -23,7 +23,7 @@ mkdir -p $O
 STEPS=${STEPS:-8}
 WLS=${WLS:-"config3 config4 config2"}
 if [ "$PARITY" = "std" ]; then
-  PARITY="copydata or warp or 64_banks or small_lds or config3_flow or config4_flow or fuzz_rom_parity or hram or watchdog or instr_count or wave_shapes or irq_bank or io_edges"
+  PARITY="copydata or warp or 64_banks or small_lds or config3_flow or config4_flow or fuzz_rom_parity or hram or watchdog or instr_count or wave_shapes or irq_bank or io_edges or vram_midframe"
   PARITY_FILES=${PARITY_FILES:-"tests/test_gpu_parity.py tests/test_gpu_scale.py"}
 fi
 rc=0
