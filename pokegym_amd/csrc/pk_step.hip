@@ -436,6 +436,9 @@ __device__ __forceinline__ void bus_write_any(const Ctx& c, St& s, u32 a, u32 v)
                 s.lcd0 = setb8(s.lcd0, 24, v);
                 break;
             case 0xFF46: {  // OAM DMA: instantaneous 160-byte copy (pyboy mb.transfer_DMA)
+#ifdef PK_ABLATE_DMA
+                break;      // (diagnostic ablation build: what the copy costs, profiles/r06/ab_dma; breaks parity)
+#endif
                 if (s.npend) {
                     flush_lines(A.lat, A.lat_stride, A.screen, c.g, c.lane, c.sh, c.glane, c.env, c.gid, s.npend);
                     s.npend = 0;
