@@ -525,8 +525,8 @@ __device__ __forceinline__ void pk_write_slow(const PkStepArgs* A, u8* g, u32 la
 // pass is left).  Only when nothing can happen inside the passes: CPU running with no interrupt
 // pending, timer off, their cycles (and the next instruction's) below the next LCD event (LCD off:
 // the frame end) and inside the watchdog budget; code in staged ROM; source in staged ROM, VRAM
-// or WRAM, destination in VRAM or WRAM (no echo, OAM, HRAM or IO), disjoint; no rendered lines
-// pending.  Returns the passes run.
+// or WRAM, destination in VRAM or WRAM (no echo, OAM, HRAM or IO), disjoint; VRAM only with no
+// rendered lines pending.  Returns the passes run.
 #define PK_COPY_W0 0x0B13122Au          // 2A 12 13 0B: ld a,[hli] / ld [de],a / inc de / dec bc
 #define PK_COPY_W1A 0xF820B079u         // 79 B0 20 F8: ld a,c / or b / jr nz,-8 (pokered)
 #define PK_COPY_W1B 0xF820B178u         // 78 B1 20 F8: ld a,b / or c / jr nz,-8
@@ -543,13 +543,16 @@ __device__ __forceinline__ bool copy_ram(u32 a) { return (a - 0x8000u < 0x2000u)
 __device__ __forceinline__ u32 pk_copy_loop(St& s, const Ctx& c, u32 pc, int& slack, u32& icount) {
     const u32 cpu = s.cpu;
     if ((cpu & (CPU_CRASH | CPU_HALT | CPU_QUEUED)) | ((cpu >> 8) & (cpu >> 16) & 0x1Fu)) return 0;
-    if (s.npend | (s.tim0 & (4u << 24))) return 0;
+    if (s.tim0 & (4u << 24)) return 0;
     if (!rom_staged(s, pc) || (pc & 0x3FFFu) > 0x3FF8u) return 0;
     const u32 li = rom_lds_index(s, pc) + 4u;
     const u32* romw = reinterpret_cast<const u32*>(lds_rom);
     const u32 w1 = __builtin_amdgcn_alignbyte(romw[(li >> 2) + 1u], romw[li >> 2], li & 3u);
     if (w1 != PK_COPY_W1A && w1 != PK_COPY_W1B) return 0;
     const u32 bc = s.w0 & 0xFFFFu, de = s.w0 >> 16, hl = s.w1 & 0xFFFFu;
+    // latched lines waiting for rasterisation: a copy into VRAM goes the instruction-by-instruction
+    // way (its writes decide the flushes, pend_hit); a copy into WRAM changes nothing they read
+    if (s.npend && de < 0xA000u) return 0;
     u32 k = (bc == 0u ? 0x10000u : bc) - 1u;          // passes before the last one
     k = min(k, PK_COPY_CAP);
     // 52 cycles and 59 watchdog units per pass; the iteration's own ld a,[hli]: 8 and 9

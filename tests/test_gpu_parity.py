@@ -329,3 +329,35 @@ def test_copydata_block_path_parity(shape, monkeypatch):
     gpu, ref = _run_both(copydata_rom(), None, n, 6, 17)
     bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
     assert not bad, bad[:4]
+
+
+@pytest.mark.parametrize("small", [False, True])
+def test_sm83_kat_on_device(small, monkeypatch):
+    """The HIP K1 runs the known-answer ROM (pokegym_amd/testrom/kat.py, A values stepping by 5), one
+    group of blocks per env (64 envs): every block hash == the documented CPU's (tests/sm83_spec.py)
+    — the 8-bit ALU with carry clear and set, DAA, INC/DEC, rotates/shifts/SWAP/BIT, CPL/SCF/CCF,
+    ADD HL,BC, ADD SP,e and LD HL,SP+e — and the whole state == the oracle's; in the default kernel
+    and in the small-LDS kernel of the VecEnv sub-batches."""
+    import torch
+    from pokegym_amd.emulator import BatchedEmulator
+    from pokegym_amd.testrom import kat
+    from tests.test_sm83_kat import check_group_outputs, kernel_outputs
+    if small:
+        monkeypatch.setenv("PK_K1_SMALL", "1")
+        monkeypatch.setenv("PK_WAVE_LANES", "32")
+        monkeypatch.setenv("PK_K1_BLOCK", "256")
+    stride, n, steps = 5, 64, 24
+    rom = kat.kat_rom(stride)
+    groups = [e % 8 for e in range(n)]
+    acts = np.array([kat.GROUP_ACTION[g] for g in groups], np.uint8)
+    emu = BatchedEmulator(rom, n, render=True)
+    a = torch.from_numpy(acts).to(emu.device)
+    for _ in range(steps):
+        emu.step(a)
+    torch.cuda.synchronize()
+    states = emu.snapshot_range(0, n)
+    emu.close()
+    assert check_group_outputs(kernel_outputs(rom, states), groups, stride) == []
+    ref, _ = oracle.batch_run(rom, None, np.repeat(acts[None, :], steps, axis=0), want_screens=False)
+    bad = [e for e in range(n) if states[e].tobytes() != ref[e].tobytes()]
+    assert not bad, bad[:8]
