@@ -149,3 +149,65 @@ class Fletcher:
 
     def pair(self):
         return self.h & 0xFF, self.h >> 8
+
+
+# ---- instruction timing (T-states, Pan Docs / the opcode tables): (not taken, taken) ----
+ILLEGAL = {0xD3, 0xDB, 0xDD, 0xE3, 0xE4, 0xEB, 0xEC, 0xED, 0xF4, 0xFC, 0xFD}
+
+
+def cycles(op: int):
+    """T-states of base opcode op as (cycles, cycles when a condition holds) — equal for the
+    unconditional ones; None for the illegal opcodes and the CB prefix (see cb_cycles)."""
+    if op in ILLEGAL or op == 0xCB:
+        return None
+    hi, lo = op >> 6, op & 7
+    if 0x40 <= op < 0x80:                       # LD r,r' / LD r,(HL) / LD (HL),r / HALT
+        if op == 0x76:
+            return (4, 4)
+        return (8, 8) if (lo == 6 or (op >> 3) & 7 == 6) else (4, 4)
+    if 0x80 <= op < 0xC0:                       # ALU A,r / A,(HL)
+        return (8, 8) if lo == 6 else (4, 4)
+    fixed = {
+        0x00: 4, 0x10: 4, 0x76: 4, 0xF3: 4, 0xFB: 4, 0x27: 4, 0x2F: 4, 0x37: 4, 0x3F: 4,
+        0x07: 4, 0x0F: 4, 0x17: 4, 0x1F: 4,
+        0x02: 8, 0x12: 8, 0x22: 8, 0x32: 8, 0x0A: 8, 0x1A: 8, 0x2A: 8, 0x3A: 8,
+        0x08: 20, 0xE0: 12, 0xF0: 12, 0xE2: 8, 0xF2: 8, 0xEA: 16, 0xFA: 16,
+        0xF8: 12, 0xF9: 8, 0xE8: 16, 0x36: 12, 0x34: 12, 0x35: 12,
+        0xC3: 16, 0xE9: 4, 0x18: 12, 0xCD: 24, 0xC9: 16, 0xD9: 16,
+    }
+    if op in fixed:
+        return (fixed[op], fixed[op])
+    if hi == 0:
+        if lo == 1:
+            return (12, 12) if op & 0x08 == 0 else (8, 8)          # LD rr,nn / ADD HL,rr
+        if lo == 3:
+            return (8, 8)                                           # INC / DEC rr
+        if lo in (4, 5):
+            return (4, 4)                                           # INC / DEC r
+        if lo == 6:
+            return (8, 8)                                           # LD r,n
+        if lo == 0 and op in (0x20, 0x28, 0x30, 0x38):
+            return (8, 12)                                          # JR cc,e
+    if hi == 3:
+        if lo == 6:
+            return (8, 8)                                           # ALU A,n
+        if lo == 7:
+            return (16, 16)                                         # RST
+        if lo == 5:
+            return (16, 16)                                         # PUSH
+        if lo == 1:
+            return (12, 12)                                         # POP
+        if op in (0xC2, 0xCA, 0xD2, 0xDA):
+            return (12, 16)                                         # JP cc,nn
+        if op in (0xC4, 0xCC, 0xD4, 0xDC):
+            return (12, 24)                                         # CALL cc,nn
+        if op in (0xC0, 0xC8, 0xD0, 0xD8):
+            return (8, 20)                                          # RET cc
+    raise KeyError(f"no documented timing for {op:02X}")
+
+
+def cb_cycles(op: int) -> int:
+    """T-states of CB-prefixed op: 8 on a register, 16 on (HL), BIT n,(HL) 12."""
+    if op & 7 != 6:
+        return 8
+    return 12 if 0x40 <= op < 0x80 else 16

@@ -42,6 +42,16 @@ int main() {
         for (uint32_t b : probes) bad += (vperm(b, b, e[PK_UE_V]) & 0xFFu) != PK_U2_NONE;
     }
     printf("nofuse %u bad %u\n", nofuse, bad);
+    // cycles: base and extra-when-taken of every primary entry (V word, T-states), then the
+    // secondary-op table's length and cycles per opcode
+    for (int i = 0; i < 512; i++) {
+        const uint32_t v = t[(size_t)i * PK_UE_WORDS + PK_UE_V];
+        printf("cyc%d %u\n", i, ((v >> 16) & 0xFFu) | (((v >> 24) & 0xFFu) << 8));
+    }
+    for (int op = 0; op < 256; op++) {
+        const uint32_t y = t[PK_UC_U2 + (size_t)op * PK_U2_WORDS + 1];
+        printf("u2_%d %u\n", op, (y & 3u) | (((y >> PK_U2B_CYC) & 15u) << 8));
+    }
     return 0;
 }
 """
@@ -63,3 +73,31 @@ def test_u2_none_entry_is_empty(table_report):
 
 def test_nofuse_primaries_select_the_empty_entry(table_report):
     assert table_report["nofuse"] >= 40 and table_report["bad"] == 0
+
+
+def test_cycles_match_the_documented_cpu(table_report):
+    """Every primary microcode entry's cycles (V word: base, + extra when the condition holds) and
+    every secondary op's cycles (the fused successor; JR not taken — taken adds 4 in pk_step.hip)
+    == the published opcode timing (tests/sm83_spec.py cycles / cb_cycles)."""
+    from tests import sm83_spec as S
+    bad = []
+    for op in range(256):
+        doc = S.cycles(op)
+        if doc is None:
+            continue
+        v = table_report[f"cyc{op}"]
+        base, extra = v & 0xFF, v >> 8
+        if (base, base + extra) != doc:
+            bad.append((f"{op:02X}", (base, base + extra), doc))
+        u2 = table_report[f"u2_{op}"]
+        if u2 & 3:
+            c2 = u2 >> 8
+            # a fused JR: the table holds the not-taken cycles, a taken one (JR e always) adds 4
+            jr = op in (0x18, 0x20, 0x28, 0x30, 0x38)
+            if (jr and (c2 + 4 != doc[1] or (op != 0x18 and c2 != doc[0]))) or (not jr and c2 != doc[0]):
+                bad.append((f"u2 {op:02X}", c2, doc))
+    for op in range(256):
+        v = table_report[f"cyc{256 + op}"]
+        if (v & 0xFF, v >> 8) != (S.cb_cycles(op), 0):
+            bad.append((f"CB {op:02X}", (v & 0xFF, v >> 8), S.cb_cycles(op)))
+    assert not bad, bad[:10]
