@@ -2,6 +2,7 @@
 
 Public surface:
   pokegym_amd.emulator.BatchedEmulator   device-resident batch of emulators (C ABI wrapper)
+  pokegym_amd.env.Base                   the reference's Base: emulator surface, no reward stack (environment.py:89)
   pokegym_amd.env.Environment            per-env Gymnasium-shaped surface (environment.py:436)
   pokegym_amd.env.VecEnv                 PufferLib-shaped batched surface
 """
@@ -13,5 +14,5 @@ def __getattr__(name):
     (pokegym/__init__.py); loaded on first use so importing the package needs no GPU."""
     if name in ("Environment", "Base", "VecEnv"):
         from . import env
-        return env.VecEnv if name == "VecEnv" else env.Environment
+        return getattr(env, name)
     raise AttributeError(name)

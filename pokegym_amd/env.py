@@ -50,37 +50,42 @@ def _read(path_or_bytes):
         return f.read()
 
 
-class Environment:
-    """One env (a single emulator lane).  Functionally the reference env; for throughput use
-    VecEnv, which steps thousands of envs per kernel launch."""
+class Base:
+    """pokegym.environment.Base (environment.py:89-434): the emulator surface without the reward
+    stack — step(action) runs the action and returns (render(), 0, False, False, {}) (:404-406),
+    reset() returns the current screen without touching the game (:228-230), plus the savestate,
+    screenshot and video helpers Environment inherits.  As there, the template state is kept in
+    initial_states but not loaded (make_env boots the ROM, :116-122), and render() keeps its own
+    visited-tile memory per map (:157-160, :256-272), here on the device."""
+
+    _next_id = 0
 
     def __init__(self, rom_path="pokemon_red.gb", state_path=None, headless=True, save_video=False, quiet=False,
-                 verbose=False, device: int = 0, max_episode_steps: int = 20480, reward_scale: float = 4.0, **kwargs):
-        from .emulator import BatchedEmulator
-        rom = _read(rom_path)
+                 device: int = 0, **kwargs):
         state = _read(state_path if state_path is not None else DEFAULT_STATE)
-        self.max_episode_steps, self.reward_scale = max_episode_steps, reward_scale
-        self._default_episode = (int(max_episode_steps), float(reward_scale))   # reset()'s defaults
-        self.emu = BatchedEmulator(rom, 1, state=state, device=device, render=True, reward=True,
-                                   max_episode_steps=max_episode_steps, reward_scale=reward_scale, heatmap=True)
+        self.emu = self._emulator(_read(rom_path), state, device)
         self.observation_space = spaces.observation_space()
         self.action_space = spaces.action_space()
         self.headless = headless
-        self.initial_states = [io.BytesIO(state)]   # environment.py:119-120 (the template state)
+        self.initial_states = [io.BytesIO(state)]   # environment.py:119-122 (the template state)
         self.pokemon_center_save_states = []
         # video / screenshots (environment.py:123, :128, :140, :200-206, :1244-1249, :1340, :1616)
         self.save_video = save_video
         self.screenshot_counter = 0
         self.reset_count = 0
-        self.env_id = Environment._next_id
-        Environment._next_id += 1
+        self.env_id = Base._next_id
+        Base._next_id += 1
         self.s_path = Path(kwargs["s_path"]) if "s_path" in kwargs else _session_path(self.env_id)
         self._recorder = None
         if save_video:
             from .video import FrameRecorder
             self._recorder = FrameRecorder(self.emu, [0])
+        self.screen_memory = {}     # map -> (255, 255) u8 device tensor (environment.py:157-160)
 
-    _next_id = 0
+    def _emulator(self, rom, state, device):
+        # the ROM boots; the template state only goes into initial_states (environment.py:116-122)
+        from .emulator import BatchedEmulator
+        return BatchedEmulator(rom, 1, state=None, device=device, render=True)
 
     def video(self):
         """environment.py:408-410: the current (144, 160, 3) screen."""
@@ -120,6 +125,56 @@ class Environment:
         data = state.getvalue() if hasattr(state, "getvalue") else bytes(state)
         self.emu.load_env(0, data)
 
+    def reset(self, seed=None, options=None):
+        """environment.py:228-230: the current screen, the game untouched (seeding is not supported)."""
+        return self.video(), {}
+
+    def step(self, action):
+        """environment.py:404-406: run the action (the same press / release schedule as
+        Environment.step, pyboy_binding.py:71-91), then (render(), 0, False, False, {})."""
+        a = torch.tensor([int(action)], dtype=torch.uint8, device=self.emu.device)
+        self.emu.step(a)
+        return self.render(), 0, False, False, {}
+
+    def render(self):
+        """environment.py:256-272 (+ get_fixed_window :233-254): mark the player's tile in this
+        map's memory, then the screen at half resolution (3 channels) beside the (72, 80) window of
+        that memory centred on the player, zero-padded past the 255 x 255 edge."""
+        pos = self.emu.peek(0, 0xD35E, 5)               # ram_map.position: D35E map, D361 y, D362 x
+        r, c, m = pos[3], pos[4], min(pos[0], 247)
+        mm = self.screen_memory.get(m)
+        if mm is None:
+            mm = self.screen_memory[m] = torch.zeros((255, 255), dtype=torch.uint8, device=self.emu.device)
+        if r <= 254 and c <= 254:
+            mm[r, c] = 255
+        win = torch.zeros((72, 80), dtype=torch.uint8, device=self.emu.device)
+        y0, y1, x0, x1 = max(0, r - 36), min(255, r + 36), max(0, c - 40), min(255, c + 40)
+        if y0 < y1 and x0 < x1:
+            win[y0 - r + 36:y1 - r + 36, x0 - c + 40:x1 - c + 40] = mm[y0:y1, x0:x1]
+        half = self.emu.screen[0, ::2, ::2]
+        return torch.stack((half, half, half, win), dim=2).cpu().numpy()
+
+    def close(self):
+        self.emu.close()
+
+
+class Environment(Base):
+    """One env (a single emulator lane) with pokegym's reward stack (environment.py:436-1812).
+    Functionally the reference env; for throughput use VecEnv, which steps thousands of envs per
+    kernel launch."""
+
+    def __init__(self, rom_path="pokemon_red.gb", state_path=None, headless=True, save_video=False, quiet=False,
+                 verbose=False, device: int = 0, max_episode_steps: int = 20480, reward_scale: float = 4.0, **kwargs):
+        self.max_episode_steps, self.reward_scale = max_episode_steps, reward_scale
+        self._default_episode = (int(max_episode_steps), float(reward_scale))   # reset()'s defaults
+        super().__init__(rom_path, state_path, headless, save_video, quiet, device=device, **kwargs)
+        self.screen_memory = None   # the reward stack's observation keeps it on the device (K3)
+
+    def _emulator(self, rom, state, device):
+        from .emulator import BatchedEmulator
+        return BatchedEmulator(rom, 1, state=state, device=device, render=True, reward=True,
+                               max_episode_steps=self.max_episode_steps, reward_scale=self.reward_scale, heatmap=True)
+
     def reset(self, seed=None, options=None, max_episode_steps=None, reward_scale=None):
         """environment.py:1233-1334 (seeding is not supported, as in the reference).  As there, every
         reset sets max_episode_steps / reward_scale from its arguments (:1258-1259): an argument left
@@ -157,10 +212,8 @@ class Environment:
         return obs[0].cpu().numpy(), float(rew[0].item()), done, done, info
 
     def render(self):
+        """Base.render's observation as the reward stack's K3 built it for the last step / reset."""
         return self.emu.obs[0].cpu().numpy()
-
-    def close(self):
-        self.emu.close()
 
 
 class VecEnv:

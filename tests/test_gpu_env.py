@@ -66,6 +66,98 @@ def test_environment_200_steps_vs_oracle():
     env.close()
 
 
+def test_base_and_environment_exports():
+    """`from pokegym import Base, Environment` (pokegym/__init__.py): two classes, Environment(Base)
+    (environment.py:89, :436), with the reference's Base methods."""
+    import pokegym_amd
+    from pokegym_amd import env
+    assert pokegym_amd.Base is env.Base and pokegym_amd.Environment is env.Environment
+    assert issubclass(env.Environment, env.Base) and env.Base is not env.Environment
+    for m in ("save_screenshot", "save_state", "load_pokemon_center_state", "load_last_state", "load_first_state",
+              "load_random_state", "reset", "render", "step", "video", "close"):
+        assert callable(getattr(env.Base, m)), m
+
+
+def _base_vs_oracle(env, rom, steps):
+    """pokegym's Base (environment.py:89-434): the ROM boots (the template state is not loaded,
+    :116-122), reset() returns the screen untouched (:228-230), and each step(a) is the action alone —
+    no reward stack, so no RAM writes of its own — returning (render(), 0, False, False, {})
+    (:404-406), render() the half-size screen beside this map's visited-tile window (:256-272).
+    Against the oracle emulator + oracle/reward.render with a fresh per-map memory, for seeded
+    actions: obs and WRAM every step, the v9 state at the start and the end.  The test ROMs keep
+    no pokered position, so before each step the player's (map, y, x) at D35E / D361 / D362 are set
+    in both — walks with jumps, three maps, the window's edges (0, 254, 255) and maps past 247."""
+    from oracle import oracle as O
+    from oracle import reward as R
+    grey = np.array([0xFF, 0x99, 0x55, 0x00], np.uint8)
+    gb = O.GB(rom)
+    assert env.emu.snapshot(0) == gb.save_state()
+
+    class Bus:
+        def r(self, a):
+            return gb.read(a)
+
+        def w(self, a, v):
+            raise AssertionError("Base.render writes no game memory")
+
+    st, bus = R.EnvState(), Bus()
+    scr, info = env.reset()
+    assert info == {} and np.array_equal(scr, np.repeat(grey[gb.screen()][..., None], 3, axis=2))
+    rng = np.random.default_rng(7)
+    maps = set()
+    m, y, x = 3, 10, 10
+    for t in range(steps):
+        a = int(rng.integers(0, 8))
+        k = int(rng.integers(0, 10))
+        if k == 0:
+            m = int(rng.choice([3, 12, 250]))
+        elif k == 1:
+            y, x = (int(v) for v in rng.choice([0, 1, 36, 200, 218, 219, 254, 255], 2))
+        else:
+            y, x = (y + int(rng.integers(-1, 2))) & 0xFF, (x + int(rng.integers(-1, 2))) & 0xFF
+        for addr, v in ((0xD35E, m), (0xD361, y), (0xD362, x)):
+            env.emu.poke(0, addr, bytes([v]))
+            gb.write(addr, v)
+        obs, rew, term, trunc, info = env.step(a)
+        gb.run_action(a)
+        want = R.render(st, bus, grey[gb.screen()])
+        maps.add(gb.read(0xD35E))
+        assert (rew, term, trunc, info) == (0, False, False, {})
+        assert obs.shape == (72, 80, 4) and np.array_equal(obs, want), f"step {t + 1}: obs differs"
+        assert np.array_equal(env.emu.peek(0, 0xC000, 0x2000), gb.wram().tobytes()), f"step {t + 1}: WRAM differs"
+    assert np.array_equal(env.render(), want)     # render() again: same tile, same window
+    assert env.emu.snapshot(0) == gb.save_state()
+    return maps
+
+
+def test_hostsim_base_vs_oracle():
+    """Base's host logic (boot, reset, step, the device-side render) over the host-simulated kernels."""
+    from pokegym_amd.env import Base
+    from pokegym_amd.testrom.game import game_rom
+    from tests.hostsim.emulator import HostsimEmulator
+
+    class HostBase(Base):
+        def _emulator(self, rom, state, device):
+            return HostsimEmulator(rom, 1, state=None, render=True)
+
+    rom = game_rom()
+    env = HostBase(rom_path=rom)
+    _base_vs_oracle(env, rom, 30)
+    env.close()
+
+
+@pytest.mark.gpu
+def test_base_steps_vs_oracle():
+    """_base_vs_oracle on the HIP path, 120 steps of pkbench."""
+    from pokegym_amd.env import Base
+    from pokegym_amd.testrom.game import game_rom
+    rom = game_rom()
+    env = Base(rom_path=rom)
+    maps = _base_vs_oracle(env, rom, 120)
+    assert len(maps) == 3, maps
+    env.close()
+
+
 @pytest.mark.gpu
 def test_vecenv_steps_and_autoresets():
     import torch
