@@ -949,18 +949,6 @@ static __device__ void pk_check_lane(const St& s, const Ctx& c, int slack, u32 p
 }
 #endif
 
-// progress-ranked wave priority (see K1's `fit`): the quarter of the step's frames the wave's
-// slowest running lane is in -> s_setprio 3, 2, 1, 0 (out of line: a call every 64 iterations)
-static __device__ __noinline__ void pk_fair_prio(u32 frames, u32 frame) {
-    u32 mf = 0;   // frame of the wave's slowest running lane (frames < 256)
-    for (u32 b = 128u; b; b >>= 1) mf += sel(__builtin_amdgcn_ballot_w64(frame < mf + b) == 0ull, b, 0u);
-    const u32 q4 = mf * 4u;
-    if (q4 >= 3u * frames) __builtin_amdgcn_s_setprio(0);
-    else if (q4 >= 2u * frames) __builtin_amdgcn_s_setprio(1);
-    else if (q4 >= frames) __builtin_amdgcn_s_setprio(2);
-    else __builtin_amdgcn_s_setprio(3);
-}
-
 // ---------------------------------------------------------------------------------------------
 // K1
 // PRIO: the launch runs two waves per SIMD (A.prio, chosen by the host), and K1 raises a wave's
@@ -1073,21 +1061,6 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
     // stage anyway, are fetched there again), so the loop top tests one value for both
     u32 pbytes = PK_COPY_W0;
     uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0, p2 = p0, p3 = p0;
-    // progress-ranked wave priority (A.fair; not with the PRIO variant, which sets its own).  Two K1
-    // workgroups share each CU (the small-LDS kernel, or two sub-batch launches), so each SIMD holds
-    // two waves, and it issues the OLDER one whenever both are ready: that wave runs almost as if
-    // alone and finishes ~30 % sooner, and the SIMD then runs the younger alone, latency-bound, at
-    // about half its two-wave rate (profiles/r06/wavetime: a whole-handle launch's first-dispatched
-    // workgroup on each CU takes 38 ms, the second 53 ms, for the same work).  Every 64 iterations a
-    // wave sets its issue priority from its own progress — 3 in the first quarter of the step's
-    // frames at its slowest running lane, down to 0 in the last — so a wave that is behind wins the
-    // issue ties until it reaches its partner's quarter.  Scheduling only: nothing emulated depends on it.
-    // Measured (profiles/r06/ab_fair): a whole-handle launch +10 %; the VecEnv shapes the bench
-    // lines run, whose two sub-batch launches already fill each other's tails, within +-1 %.
-    // (fit counts iterations while on; off, it stays at 1 and never reaches a multiple of 64)
-    u32 fit = (!PRIO && A.fair) ? 0u : 1u;
-    const u32 finc = (!PRIO && A.fair) ? 1u : 0u;
-    if (!PRIO && A.fair) __builtin_amdgcn_s_setprio(3);
 #ifdef PK_STAMP
     uint64_t st_acc[PK_NSTAMP] = {}, st_prev = __builtin_amdgcn_s_memtime(), st_iter = 0;
 #endif
@@ -1492,8 +1465,6 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
             }
             s.lim = tick_lim(s, slack);
         }
-        fit += finc;
-        if (PK_RARE((__builtin_amdgcn_readfirstlane(fit) & 63u) == 0u)) pk_fair_prio(A.frames, frame);
         PK_ITER(env, ev);
         PK_ITER_OP(env, sel(exec, sel((bytes & 0xFFu) == 0xCBu, 256u + ((bytes >> 8) & 0xFFu), bytes & 0xFFu),
                             sel(dispatch, PK_UC_INT, sel(doint, PK_UC_NOP0, PK_UC_IDLE))));
