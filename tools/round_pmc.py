@@ -23,6 +23,17 @@ def per_dispatch(d, kernel):
     return vals
 
 
+def sane(vals):
+    """Drop dispatches whose SQ_WAVES is not the pass's median: a launch of fixed geometry has one wave
+    count, and rocprofv3 once reported a K1 dispatch of 1,024 waves as 2,048 (profiles/r06q: every
+    counter of that row doubled) — such a row would skew the means."""
+    w = sorted(v["SQ_WAVES"] for v in vals.values() if "SQ_WAVES" in v)
+    if not w:
+        return vals
+    med = w[len(w) // 2]
+    return {k: v for k, v in vals.items() if v.get("SQ_WAVES", med) == med}
+
+
 def mean(vals, key, skip_first=True):
     ids = sorted(vals)
     if skip_first and len(ids) > 1:
@@ -40,7 +51,7 @@ def main():
     fs, ws = gib / cf, gib / cw          # bytes per FETCH_SIZE / WRITE_SIZE unit (3 copies averaged)
     f = per_dispatch(os.path.join(D, "fetch"), "pk_step_kernel")
     w = per_dispatch(os.path.join(D, "write"), "pk_step_kernel")
-    v = per_dispatch(os.path.join(D, "valu"), "pk_step_kernel")
+    v = sane(per_dispatch(os.path.join(D, "valu"), "pk_step_kernel"))
     rd, wr = mean(f, "FETCH_SIZE") * fs, mean(w, "WRITE_SIZE") * ws
     # rocprofv3's VALUBusy: 100 * sum(SQ_ACTIVE_INST_VALU) / CU_NUM / max(GRBM_GUI_ACTIVE); the
     # per-dispatch GRBM_GUI_ACTIVE here is summed over the 8 XCDs, so max = sum / 8
@@ -59,7 +70,7 @@ def main():
     # (SQ_INSTS_* / SQ_WAVES / the instructions one env executes in the launch)
     issue = None
     if os.path.isdir(os.path.join(D, "issue")):
-        q = per_dispatch(os.path.join(D, "issue"), "pk_step_kernel")
+        q = sane(per_dispatch(os.path.join(D, "issue"), "pk_step_kernel"))
         ib = json.loads(open(os.path.join(D, "issue_bench.json")).read().strip().splitlines()[-1])
         ipe = ib["instr_per_env_step"]
         waves = mean(q, "SQ_WAVES")
