@@ -264,7 +264,6 @@ struct pk_handle {
     // reset lists (pk_list_kernel): [0] reload count, [1] obs count, then npad reload ids, npad obs ids
     uint32_t* lists = nullptr;
     unsigned long long* dbg = nullptr;  // K1 phase-cycle counters of a -DPK_STAMP build
-    uint32_t tailprio = 0;     // K1 tail priority (PK_TAILPRIO=k: lanes left at which a wave takes priority 3)
     double* info = nullptr;       // [PK_INFO_NFIELDS][npad]
     uint8_t* info_flag = nullptr; // [npad]
     int32_t* heat = nullptr;      // [npad][444 * 436] (PK_F_HEATMAP)
@@ -362,7 +361,6 @@ int pk_create(const pk_config* cfg, pk_handle** out) {
         }
         if (const char* pr = getenv("PK_K1_PRIO")) h->k1_prio = atoi(pr) ? 1 : 0;
         if (const char* sm = getenv("PK_K1_SMALL")) h->k1_small = atoi(sm) ? 1 : 0;
-        if (const char* tp = getenv("PK_TAILPRIO")) h->tailprio = (uint32_t)atoi(tp);
         // image interleave = K1's envs per wave for this handle (no 64-byte line shared by two
         // waves; a wave's lanes share one sub-block base).  PK_ILV overrides it with any power of
         // two <= 64: narrower than the wave puts one wave's envs in several sub-blocks (K1 reaches
@@ -682,7 +680,6 @@ static PkStepArgs step_args(pk_handle* h, const uint8_t* actions, uint32_t env0,
     k1_shape(h, small, a.wave_lanes, a.block, a.prio);
     a.simds = h->simds;
     a.dbg = h->dbg;
-    a.tailprio = h->tailprio;
     a.env0 = env0; a.env1 = env1;
     a.ilv_sh = h->ilv_sh;
     return a;

@@ -152,7 +152,6 @@ struct PkStepArgs {
     uint32_t ilv_sh;          // image interleave: 1 << ilv_sh envs (pk_img_off)
     uint32_t small;           // launch the small-LDS K1 (pk_launch_step_small)
     uint32_t all_staged;      // every ROM bank is staged in this kernel's LDS slots (the ALL instance)
-    uint32_t tailprio;        // K1 tail priority: a wave with this many lanes or fewer left takes s_setprio 3 (0 = off)
 };
 
 struct PkResetArgs {

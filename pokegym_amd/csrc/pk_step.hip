@@ -120,7 +120,6 @@ struct PkLds {
     u32 u2[PK_UC_WORDS - PK_UC_U2];                   // secondary ops (small-LDS kernel: base in the 16-bit offset)
     u32 uc[PK_UC_U2];                                 // microcode
     int8_t slot[128];                                 // bank -> slot
-    u8 run[PK_K1_MAX_THREADS];                        // 1 while the thread's env is still stepping (pk_tail_prio)
 };
 __shared__ __attribute__((aligned(16))) PkLds pk_lds;
 #define lds_rom pk_lds.rom
@@ -950,25 +949,6 @@ static __device__ void pk_check_lane(const St& s, const Ctx& c, int slack, u32 p
 }
 #endif
 
-// Tail priority (A.tailprio = k > 0; not with the PRIO variant, which sets its own): the launch
-// lasts as long as its slowest env, and that env's wave runs on with a few lanes long after the
-// others are done (an env in pkbench's door warp).  When one of a wave's
-// lanes finishes its last frame, the wave counts its lanes still stepping (one LDS byte per thread,
-// written by the thread alone: no atomics) and, with k or fewer left, takes issue priority 3 over
-// its SIMD's other wave for the rest of the launch.  Called from the frame-end block with the
-// finishing lanes active.  Scheduling only: nothing emulated depends on it.
-static __device__ __noinline__ void pk_tail_prio(u32 k) {
-    pk_lds.run[threadIdx.x] = 0;
-    const uint4* r = reinterpret_cast<const uint4*>(pk_lds.run + (threadIdx.x & ~63u));
-    u32 n = 0;
-    for (u32 i = 0; i < 4u; i++) {
-        const uint4 v = r[i];
-        n += ((v.x * 0x01010101u) >> 24) + ((v.y * 0x01010101u) >> 24) + ((v.z * 0x01010101u) >> 24)
-           + ((v.w * 0x01010101u) >> 24);
-    }
-    if (__builtin_amdgcn_readfirstlane(n) <= k) __builtin_amdgcn_s_setprio(3);
-}
-
 // ---------------------------------------------------------------------------------------------
 // K1
 // PRIO: the launch runs two waves per SIMD (A.prio, chosen by the host), and K1 raises a wave's
@@ -991,7 +971,6 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         for (u32 i = threadIdx.x; i < 0x4000u / 16u; i += blockDim.x) dst[i] = src[i];
     }
     __syncthreads();
-    pk_lds.run[threadIdx.x] = 0;   // (pk_tail_prio) set below for the threads that step an env
 
     // thread -> env: the first wave_lanes lanes of each wave carry envs (fewer envs per wave =
     // more waves per SIMD for the same env count); the RAM layout is unchanged.
@@ -1058,7 +1037,6 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
     u32 icount = 0;
 
     const bool active = env < A.env1;
-    pk_lds.run[threadIdx.x] = active ? 1u : 0u;
     u32 frame = active ? 0u : A.frames;
     const u32 action = active ? A.actions[env] : 8u;   // actions: full-size [n] array
     // pyboy_binding.py:7-40 ACTIONS: Down Left Right Up A B Start Select -> interaction buttons
@@ -1482,7 +1460,6 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
                 s.frame_done = 0;
                 slack = (int)(16u * FRAME_CYCLES);
                 frame += 1u;
-                if (!PRIO && A.tailprio && frame == A.frames) pk_tail_prio(A.tailprio);
                 if (frame == A.release_frame && btn != 0xFFu) key_event(s, btn, false);
                 s.render = (A.render_last && frame + 1u == A.frames) ? 1u : 0u;
             }
