@@ -632,6 +632,33 @@ __device__ __forceinline__ u32 pk_poll_loop(St& s, const Ctx& c, u32 pc, u32 byt
     return k;
 }
 
+// The OAM-DMA wait: pokered's hDMARoutine (copied to HRAM, run from the VBlank handler every frame)
+// starts the DMA and waits 160 us with
+//     ld a,$28 / dec a / jr nz,-3
+// — 40 passes of 16 cycles that change only A, F and the clock.  The passes that jump back (A stays
+// nonzero) run here in one step, up to the next LCD event, under the block copy's conditions (CPU
+// running with nothing pending, timer off, inside the watchdog budget); the iteration then executes
+// the next pass as usual.  The code may be anywhere (the prefetched bytes identify it: HRAM here).
+// Returns the passes skipped.
+#define PK_DEC_W0 0x00FD203Du           // 3D 20 FD: dec a / jr nz,-3
+__device__ __forceinline__ u32 pk_dec_loop(St& s, int& slack, u32& icount) {
+    const u32 cpu = s.cpu;
+    if ((cpu & (CPU_CRASH | CPU_HALT | CPU_QUEUED)) | ((cpu >> 8) & (cpu >> 16) & 0x1Fu)) return 0;
+    if (s.tim0 & (4u << 24)) return 0;
+    const u32 a = s.w1 >> 24, c0 = s.clock, lim = sel(s.lcd0 & 0x80u, s.target, FRAME_CYCLES);
+    if (lim <= c0 || slack < 18) return 0;
+    u32 k = (a == 0u ? 256u : a) - 1u;             // passes whose dec leaves A != 0 (jr taken)
+    k = min(k, (lim - c0 - 1u) / 16u);             // passes end before the event
+    k = min(k, (u32)(slack - 18) / 18u);           // 16 cycles + 2 instructions each
+    if (k == 0u) return 0;
+    const u32 na = (a - k) & 0xFFu;                // != 0
+    // the last dec's flags: Z 0, N 1, H from the borrow out of bit 4 (the old low nibble was 0), C kept
+    const u32 f = (bfe8(s.w1, 16) & 0x10u) | 0x40u | sel(((na + 1u) & 0xFu) == 0u, 0x20u, 0u);
+    s.w1 = (s.w1 & 0xFFFFu) | (f << 16) | (na << 24);
+    pk_skip(s, slack, icount, 16u * k, 2u * k);
+    return k;
+}
+
 // ---------------------------------------------------------------------------------------------
 // One emulated instruction's execution: address, operand reads, fused datapath, control
 // (pk_exec) and memory writes (pk_write), the same straight-line all-units sequence in every lane.
@@ -1086,7 +1113,8 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         // the three rare stages of the loop top (interrupts / HALT, a fetch that was not prefetched,
         // a block-copy or LY-poll loop at pc) sit behind one test: the common path pays one branch
         const bool fe_rare = (cpu0 & (CPU_CRASH | CPU_HALT | CPU_QUEUED | CPU_PEND)) != 0u;
-        const bool loop_at = (pbytes == PK_COPY_W0) | ((pbytes & 0x00FFFFFFu) == PK_POLL_W0);
+        const u32 pb3 = pbytes & 0x00FFFFFFu;
+        const bool loop_at = (pbytes == PK_COPY_W0) | (pb3 == PK_POLL_W0) | (pb3 == PK_DEC_W0);
         bool pf = true;   // prefetched (iteration statistics only)
         if (PK_RARE(fe_rare | loop_at)) {
         pf = !fe_rare & (pbytes != PK_COPY_W0);
@@ -1149,11 +1177,14 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         // ---------------- block copy and LY poll (pk_copy_loop, pk_poll_loop) ----------------
         // whole passes of the loop run here; the iteration then executes the next pass's first
         // instruction as usual (the loop's first bytes identify it: no INT pseudo-op has them)
-        if ((bytes == PK_COPY_W0) | ((bytes & 0x00FFFFFFu) == PK_POLL_W0)) {
+        if ((bytes == PK_COPY_W0) | ((bytes & 0x00FFFFFFu) == PK_POLL_W0) | ((bytes & 0x00FFFFFFu) == PK_DEC_W0)) {
             if (exec) PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, bytes & 0xFFu);
             if (bytes == PK_COPY_W0) {
                 const u32 k = pk_copy_loop(s, c, pc, slack, icount);
                 if (k) PK_TRACE_SKIP(env, pc, k, 7u);
+            } else if ((bytes & 0x00FFFFFFu) == PK_DEC_W0) {
+                const u32 k = exec ? pk_dec_loop(s, slack, icount) : 0u;
+                if (k) PK_TRACE_SKIP(env, pc, k, 2u);
             } else {
                 const u32 k = pk_poll_loop(s, c, pc, bytes, slack, icount);
                 if (k) PK_TRACE_SKIP(env, pc, k, 3u);
@@ -1165,7 +1196,7 @@ __global__ void __launch_bounds__(PK_K1_MAX_THREADS) PK_K1_KERNEL(PkStepArgs A) 
         icount += 1u;   // (the rare loop-top stage takes it back for an interrupt dispatch / idle iteration)
         ev |= sel(exec, PK_EV_EXEC | sel((bytes & 0xFFu) == 0xCBu, PK_EV_CB, 0u), 0u) | sel(pf, PK_EV_F_LDS, 0u)
             | sel(dispatch, PK_EV_INT, 0u) | sel(!exec && !dispatch, PK_EV_IDLE, 0u);
-        if (exec && !((bytes == PK_COPY_W0) | ((bytes & 0x00FFFFFFu) == PK_POLL_W0)))
+        if (exec && !((bytes == PK_COPY_W0) | ((bytes & 0x00FFFFFFu) == PK_POLL_W0) | ((bytes & 0x00FFFFFFu) == PK_DEC_W0)))
             PK_TRACE(env, pc, s.w0, perm(s.w1, s.w1, 0x02030100u), s.sp, bytes & 0xFFu);
         const Mc m = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y, e2.z, e2.w, e3.x, e3.y, e3.z, e3.w};
         const u32 D = m.D;

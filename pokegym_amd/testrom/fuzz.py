@@ -344,6 +344,45 @@ def irq_bank_rom(n_banks: int = 8) -> bytes:
     return build_rom("\n".join(L), n_banks=n_banks, title="IRQBANK")
 
 
+def dma_wait_rom() -> bytes:
+    """pokered's OAM-DMA wait loop (`dec a / jr nz,-3`), which K1 runs in whole passes at once
+    (pk_step.hip pk_dec_loop): from HRAM (where pokered's hDMARoutine runs it) and from ROM, with A
+    from the joypad and a pass counter (0 = 256 passes and 1 = none to skip included), carry set or
+    clear on entry (the loop keeps it), the timer on in half of the stretches, STAT mode-0 and
+    VBlank interrupts enabled or not and IME on or off — interrupts dispatch inside the loop, their
+    handlers keep A and F.  After each loop A, F and the handler counts go into WRAM 0xC030-0xC04F."""
+    L = ["section 0",
+         "org $0040", "jp h_0", "org $0048", "jp h_1", "org $0050", "jp h_2",
+         "org $0100", "nop", "jp start", "org $0150",
+         "start:", "di", "ld sp, $dff0", "ld a, $e3", "ldh [$40], a",
+         "ld hl, rom_wait", "ld de, $ff80", "ld b, 4",
+         ".cp:", "ld a, [hl+]", "ld [de], a", "inc de", "dec b", "jr nz, .cp",
+         "main:",
+         "ld a, [$c030]", "inc a", "ld [$c030], a", "ld b, a",
+         "and $08", "rrca", "or $01", "ldh [$07], a",            # timer on (TAC 5) / off (TAC 1)
+         "ld a, b", "and $10", "rrca", "ldh [$41], a",           # STAT mode-0 interrupt on / off
+         "ld a, b", "and $07", "or $01", "ldh [$ff], a",         # IE: VBlank, + STAT, + timer
+         "ld a, $10", "ldh [$00], a", "ldh a, [$00]", "ldh a, [$00]", "xor b", "ld c, a",
+         "ld a, b", "and $20", "jr z, .di", "ei", "jr .go", ".di:", "di", ".go:",
+         "ld a, b", "and $07", "jr nz, .ab",
+         "ld a, b", "and $08", "jr .set",                         # A = 0 (256 passes) or 8
+         ".ab:", "ld a, c", "swap a", "xor b",
+         ".set:", "ld d, a",
+         "ld a, b", "rrca", "jr c, .sc", "and a", "ld a, d", "jr .call", ".sc:", "ld a, d", "scf",
+         ".call:", "bit 6, b", "jr z, .hram",
+         "call rom_wait", "jr .done",
+         ".hram:", "call $ff80",
+         ".done:", "push af", "pop hl", "di",
+         "ld a, h", "ld [$c031], a", "ld a, l", "ld [$c032], a",
+         "ld a, [$c033]", "add a, l", "ld [$c033], a",
+         "ld a, d", "ld [$c034], a",
+         "jp main",
+         "rom_wait:", "db $3d, $20, $fd, $c9"]
+    for k in range(3):
+        L += [f"h_{k}:", "push af", f"ld a, [${0xC040 + k:04x}]", "inc a", f"ld [${0xC040 + k:04x}], a", "pop af", "reti"]
+    return build_rom("\n".join(L), n_banks=2, title="DMAWAIT")
+
+
 def vram_midframe_rom() -> bytes:
     """VRAM and OAM writes in the middle of the visible frame — what K1's deferred rasteriser must
     get right: a line is latched at its mode-0 event and rasterised later (K2 at the step's end, or

@@ -279,6 +279,33 @@ def test_vram_midframe_parity(small, monkeypatch):
     assert all(np.array_equal(scr[e], grey[ref_scr[e]]) for e in range(n))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("small", [False, True])
+def test_dma_wait_parity(small, monkeypatch):
+    """pokered's OAM-DMA wait loop (dec a / jr nz) that K1 runs in whole passes (pk_step.hip
+    pk_dec_loop): from HRAM and ROM, A = 0 / 1 / any, carry in or out, timer on/off, STAT / VBlank /
+    timer interrupts dispatching inside the loop (fuzz.py dma_wait_rom); whole state vs the oracle
+    in the default kernel and in the small-LDS kernel of the VecEnv sub-batches."""
+    from pokegym_amd.testrom.fuzz import dma_wait_rom
+    if small:
+        monkeypatch.setenv("PK_K1_SMALL", "1")
+        monkeypatch.setenv("PK_WAVE_LANES", "32")
+        monkeypatch.setenv("PK_K1_BLOCK", "256")
+    import torch
+    from pokegym_amd.emulator import BatchedEmulator
+    rom, n, steps = dma_wait_rom(), 256, 6
+    actions = np.random.default_rng(23).integers(0, 9, size=(steps, n), dtype=np.uint8)
+    emu = BatchedEmulator(rom, n, render=True)
+    for t in range(steps):
+        emu.step(torch.from_numpy(actions[t]).to(emu.device))
+    torch.cuda.synchronize()
+    gpu = [emu.snapshot(e) for e in range(n)]
+    emu.close()
+    ref, _ = oracle.batch_run(rom, None, actions)
+    bad = [(e, _diff(gpu[e], ref[e].tobytes())) for e in range(n) if gpu[e] != ref[e].tobytes()]
+    assert not bad, bad[:4]
+
+
 def warp_actions(n, seed=5):
     """Actions (6, n) from the warp fixture's state: columns 0..n/2-1 the recorded actions (they
     walk through a door at step 2: pkbench's map load with the LCD off for ~5 frames), the rest

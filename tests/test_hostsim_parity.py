@@ -80,6 +80,34 @@ def test_hostsim_vram_midframe():
     assert check(vram_midframe_rom(), 32, 6, 17) == []
 
 
+def test_hostsim_dma_wait_loop():
+    """pokered's OAM-DMA wait loop (dec a / jr nz), which K1 runs in whole passes at once
+    (pk_step.hip pk_dec_loop): from HRAM and ROM, A = 0 / 1 / any, carry in or out, timer on/off,
+    STAT / VBlank / timer interrupts dispatching inside the loop (fuzz.py dma_wait_rom); whole state
+    vs the oracle.  The fast path must have run: the host simulation's trace holds its skip records."""
+    import ctypes
+    import numpy as np
+    from pokegym_amd.testrom.fuzz import dma_wait_rom
+    from tests.hostsim import sim
+    from tests.hostsim.sim import SimEmulator
+    rom = dma_wait_rom()
+    assert check(rom, 32, 4, 23) == []
+    L = sim.lib()
+    L.pk_sim_trace_enable.argtypes = [ctypes.c_uint32, ctypes.c_uint64]
+    L.pk_sim_trace_get.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+    L.pk_sim_trace_get.restype = ctypes.c_uint64
+    cap = 1 << 20
+    L.pk_sim_trace_enable(0, cap)
+    emu = SimEmulator(rom, 1)
+    for t in range(2):
+        emu.step(np.array([t], np.uint8))
+    buf = np.zeros((cap, 6), np.uint32)
+    k = L.pk_sim_trace_get(buf.ctypes.data, cap)
+    L.pk_sim_trace_enable(0xFFFFFFFF, 0)
+    skips = buf[:k][(buf[:k, 4] & 0x1FFF) == 0x1002]
+    assert len(skips) > 0 and skips[:, 1].sum() > 100
+
+
 def test_hostsim_frame_watchdog():
     """The frame watchdog: LCD switched off faster than once per frame (its clock restarts, so
     frames end on the budget), joypad-dependent passes, timer stretches with TIMA interrupts
