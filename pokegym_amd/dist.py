@@ -39,6 +39,7 @@ class EpisodeStats:
         self.ep_return = torch.zeros(n, dtype=torch.float64, device=self.device)
         self.ep_length = torch.zeros(n, dtype=torch.float64, device=self.device)
         self.summary = torch.zeros((nbatches, len(STAT_FIELDS)), dtype=torch.float64, device=self.device)
+        self.snap = torch.zeros_like(self.summary)   # rows taken at a deferred logging interval (snapshot)
 
     def update(self, rewards: torch.Tensor, done: torch.Tensor, batch: int = 0, envs: slice = slice(None)):
         """Accumulate one step of the envs `envs` (rewards/done cover exactly those envs);
@@ -57,14 +58,21 @@ class EpisodeStats:
         ret.mul_(keep)
         length.mul_(keep)
 
-    def allreduce(self, group=None, reset: bool = True) -> dict:
+    def snapshot(self, batch: int):
+        """Move sub-batch row `batch` into the snapshot and restart it, on the current stream (the
+        sub-batch's own: stream-ordered after its last update, no host sync)."""
+        self.snap[batch].copy_(self.summary[batch])
+        self.summary[batch].zero_()
+
+    def allreduce(self, group=None, reset: bool = True, snapshot: bool = False) -> dict:
         """Sum the summaries of all ranks (RCCL over xGMI when the tensors live on GPUs).  With
         reset (the default, like InfoStats) the summary restarts, so each call covers one logging
-        interval; per-env episodes in progress keep accumulating."""
-        out = self.summary.sum(dim=0)
+        interval; per-env episodes in progress keep accumulating.  snapshot=True sums the rows
+        snapshot() took instead (they were restarted then)."""
+        out = (self.snap if snapshot else self.summary).sum(dim=0)
         if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
             dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
-        if reset:
+        if reset and not snapshot:
             self.summary.zero_()
         vals = out.tolist()
         res = dict(zip(STAT_FIELDS, vals))
@@ -86,6 +94,7 @@ class InfoStats:
         self.device = torch.device(device)
         # one row per sub-batch (concurrent streams); last column = count
         self.sum = torch.zeros((nbatches, NFIELDS + 1), dtype=torch.float64, device=self.device)
+        self.snap = torch.zeros_like(self.sum)   # rows taken at a deferred logging interval (snapshot)
 
     def update(self, info: torch.Tensor, flag: torch.Tensor, batch: int = 0):
         """info: f64 (NFIELDS, m) view, flag: (m,) 0/1 of the same envs — one GEMV, no host sync."""
@@ -94,12 +103,17 @@ class InfoStats:
         row[:-1] += torch.mv(info, f)
         row[-1] += f.sum()
 
-    def allreduce(self, group=None, reset: bool = True) -> dict:
+    def snapshot(self, batch: int):
+        """As EpisodeStats.snapshot."""
+        self.snap[batch].copy_(self.sum[batch])
+        self.sum[batch].zero_()
+
+    def allreduce(self, group=None, reset: bool = True, snapshot: bool = False) -> dict:
         from .info import REWARD_FIELDS, STATS_FIELDS
-        out = self.sum.sum(dim=0)
+        out = (self.snap if snapshot else self.sum).sum(dim=0)
         if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
             dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
-        if reset:
+        if reset and not snapshot:
             self.sum.zero_()
         vals = out.tolist()
         n = vals[-1]

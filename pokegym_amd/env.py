@@ -11,7 +11,8 @@ reset(seed) -> (obs, infos); step(actions) -> (obs, rewards, terminals, truncati
 async_reset/send/recv; single_observation_space, single_action_space, num_envs.  Finished envs
 are reset inside step (their returned obs is the first obs of the next episode), stream-ordered
 with no host synchronisation; episode statistics are accumulated on the device and all-reduced
-across ranks every `log_interval` steps (pokegym_amd.dist).  For several GPUs, run one process
+across ranks every `log_interval` steps (pokegym_amd.dist; with sub-batches the record is read one
+env-step after the interval, from per-stream snapshots, so the pipeline never drains).  For several GPUs, run one process
 per GPU and build each rank's shard with `make_sharded_vecenv`.
 """
 from __future__ import annotations
@@ -288,6 +289,12 @@ class VecEnv:
         self._current: int | None = None
         self._batch_steps = 0
         self.logs_fired = 0        # logging intervals that fired (error check + all-reduce issued)
+        # deferred interval read (sub-batch pipeline): the interval's rows and error codes are
+        # snapshotted on each sub-batch stream where it fires, and read by the host num_batches
+        # recv()s later, when the last of those streams' steps is the one being received
+        self._log_wait = 0
+        self._snap_events = [torch.cuda.Event() for _ in range(self.num_batches)] if self.num_batches > 1 else []
+        self._snap_err = torch.zeros_like(self.sticky_errors) if self.sticky_errors is not None else None
 
     def _range(self, b: int) -> slice:
         return slice(b * self.batch_size, (b + 1) * self.batch_size)
@@ -322,21 +329,24 @@ class VecEnv:
             self.emu.set_episode_params(mes, rsc)
         obs = self._logical(self.emu.reset())
         self.t = 0
+        self._log_wait = 0
         if self.sticky_errors is not None:
             self.sticky_errors.zero_()
         return obs, []
 
-    def raise_if_failed(self):
-        """Raise the reference's exception for the first env that hit one since the last check."""
-        if self.sticky_errors is None:
+    def raise_if_failed(self, codes: torch.Tensor | None = None):
+        """Raise the reference's exception for the first env that hit one since the last check
+        (codes: the sticky error codes, or a snapshot of them)."""
+        codes = self.sticky_errors if codes is None else codes
+        if codes is None:
             return
-        bad = torch.nonzero(self.sticky_errors).flatten()
+        bad = torch.nonzero(codes).flatten()
         if bad.numel():
             from ._native import ERR_EXCEPTIONS
             p = int(bad[0])
-            code = int(self.sticky_errors[p])
+            code = int(codes[p])
             e = (p // self.slot) * self.batch_size + p % self.slot
-            self.sticky_errors.zero_()
+            codes.zero_()
             raise ERR_EXCEPTIONS.get(code, RuntimeError)(
                 f"env {e}: reference reward stack raises here (PK_ERR {code}); {bad.numel()} env(s) failed")
 
@@ -363,18 +373,49 @@ class VecEnv:
             self.emu.reset_range(psl.start, self.batch_size, self.emu.terminals)
         return obs, rewards, terminals, truncations
 
-    def _log(self):
+    def _log(self, deferred: bool = False):
         infos = []
-        if self.log_interval and self._batch_steps % (self.log_interval * self.num_batches) == 0:
-            # the sticky error codes and the statistics rows are written by the sub-batch streams:
-            # wait for every one of them before reading and clearing (the next send() orders its
-            # stream after these reads again through st.wait_stream(current))
-            self._join_streams()
-            self.raise_if_failed()
+        if not (self.log_interval and self._batch_steps % (self.log_interval * self.num_batches) == 0):
+            return infos
+        if deferred and self._streams:
+            # the sub-batch pipeline: no host sync here (it would drain every stream's queue).  Each
+            # stream, after its latest step, moves its statistics rows and error codes into the
+            # snapshot and restarts them; recv() reads the snapshot once the step it waits for is
+            # the last of these (_read_logs)
+            for b, st in enumerate(self._streams):
+                with torch.cuda.stream(st):
+                    self.stats.snapshot(b)
+                    if self.info_stats is not None:
+                        self.info_stats.snapshot(b)
+                    if self.sticky_errors is not None:
+                        psl = self._prange(b)
+                        self._snap_err[psl].copy_(self.sticky_errors[psl])
+                        self.sticky_errors[psl].zero_()
+                    self._snap_events[b].record(st)
             self.logs_fired += 1
-            infos = [self.stats.allreduce()]
-            if self.info_stats is not None:
-                infos[0].update(self.info_stats.allreduce())
+            self._log_wait = self.num_batches
+            return infos
+        # the sticky error codes and the statistics rows are written by the sub-batch streams:
+        # wait for every one of them before reading and clearing (the next send() orders its
+        # stream after these reads again through st.wait_stream(current))
+        self._join_streams()
+        self.raise_if_failed()
+        self.logs_fired += 1
+        infos = [self.stats.allreduce()]
+        if self.info_stats is not None:
+            infos[0].update(self.info_stats.allreduce())
+        return infos
+
+    def _read_logs(self):
+        """The deferred interval's record: wait (host) for the snapshot, raise its first error code,
+        all-reduce its rows."""
+        cur = torch.cuda.current_stream(self.device)
+        for e in self._snap_events:
+            cur.wait_event(e)
+        self.raise_if_failed(self._snap_err)
+        infos = [self.stats.allreduce(snapshot=True)]
+        if self.info_stats is not None:
+            infos[0].update(self.info_stats.allreduce(snapshot=True))
         return infos
 
     def step(self, actions):
@@ -439,7 +480,11 @@ class VecEnv:
 
     def recv(self):
         """The next finished sub-batch: (obs, rewards, terminals, truncations, infos, env_ids, masks),
-        device tensors over its batch_size envs; the current stream waits for its step (no host sync)."""
+        device tensors over its batch_size envs; the current stream waits for its step (no host sync).
+        The num_batches-th recv() after a logging interval fired reads that interval's snapshot (a
+        host wait for the streams' steps of the interval — the last of which is the one received
+        here): it raises the first reference exception an env hit, else returns the all-reduced
+        record in infos."""
         if self.num_batches == 1:
             obs, rew, term, trunc, infos = self._pending
             return obs, rew, term, trunc, infos, self.env_ids, self.masks
@@ -447,13 +492,18 @@ class VecEnv:
             raise RuntimeError("recv() called twice without send()")
         if not self._ready:
             raise RuntimeError("recv() before async_reset()")
+        logged = []
+        if self._log_wait:
+            self._log_wait -= 1
+            if self._log_wait == 0:
+                logged = self._read_logs()
         b = self._ready.pop(0)
         torch.cuda.current_stream(self.device).wait_event(self._events[b])
         self._current = b
         sl = self._range(b)
         rew, term, trunc = self._pending[b]
         obs = self.emu.obs if self.emu.reward else self.emu.screen
-        infos, self._pending_infos = getattr(self, "_pending_infos", []), []
+        infos, self._pending_infos = getattr(self, "_pending_infos", []) + logged, []
         return obs[self._prange(b)], rew, term, trunc, infos, self.env_ids[sl], self.masks[sl]
 
     def current_envs(self) -> slice:
@@ -482,7 +532,7 @@ class VecEnv:
         self._batch_steps += 1
         if self._batch_steps % self.num_batches == 0:
             self.t += 1
-        logged = self._log()
+        logged = self._log(deferred=True)
         if logged:
             self._pending_infos = logged
         self._ready.append(b)

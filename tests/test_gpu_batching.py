@@ -119,8 +119,9 @@ def test_vecenv_sub_batches_log_raises_injected_error():
     """VecEnv(256, batch_size=64) through recv/send with a logging interval: an error
     code a sub-batch step writes on its own stream is not lost to the logging interval's check and
     clear — the reference's exception (KeyError: MAP_ID_REF lookup of an unknown map id,
-    environment.py:739) is raised at the first interval after the step that hit it, and the
-    episode statistics of every sub-batch are all-reduced in each interval."""
+    environment.py:739) is raised at the first interval after the step that hit it (by the recv()
+    that reads the interval's snapshot: VecEnv._read_logs), and the episode statistics of every
+    sub-batch are all-reduced in each interval."""
     import torch
     from pokegym_amd.env import VecEnv
     from pokegym_amd.testrom.game import game_rom
@@ -132,12 +133,12 @@ def test_vecenv_sub_batches_log_raises_injected_error():
     bad_env, raised, infos_seen, sends = 70, None, [], 0
     for rnd in range(3 * log):
         for b in range(n // bs):
-            o, r, d, t, infos, ids, m = v.recv()
-            infos_seen += infos
-            if rnd == log + 1 and int(ids[0]) == 64:          # env 70 is in the second sub-batch
-                torch.cuda.synchronize()
-                v.emu.poke(v.phys(bad_env), 0xD35E, bytes([0xF8]))   # map id 248: not in MAP_ID_REF
             try:
+                o, r, d, t, infos, ids, m = v.recv()
+                infos_seen += infos
+                if rnd == log + 1 and int(ids[0]) == 64:          # env 70 is in the second sub-batch
+                    torch.cuda.synchronize()
+                    v.emu.poke(v.phys(bad_env), 0xD35E, bytes([0xF8]))   # map id 248: not in MAP_ID_REF
                 v.send(torch.randint(0, 8, (bs,), device=v.device, generator=g).to(torch.uint8))
                 sends += 1
             except KeyError as e:

@@ -173,8 +173,11 @@ def test_vecenv_padded_sub_batch_slots(monkeypatch):
 
 def test_vecenv_logging_interval_counted_where_it_fires(monkeypatch):
     """The sub-batch pipeline's logging interval (sticky-error check + statistics all-reduce) fires
-    on the send that completes every log_interval-th env-step; VecEnv.logs_fired counts it there,
-    while its record reaches the caller only with the next recv() (bench.py reports both)."""
+    on the send that completes every log_interval-th env-step: VecEnv.logs_fired counts it there,
+    and each sub-batch stream snapshots its rows and error codes after that step.  The host reads the
+    snapshot — no host sync where it fires, which would drain every stream — num_batches recv()s
+    later, when the sub-batch being received is the last one stepped before the interval; its record
+    reaches the caller with that recv (bench.py reports both counts)."""
     for name in ("Stream", "Event", "current_stream", "stream"):
         monkeypatch.setattr(torch.cuda, name, _NoStream)
     monkeypatch.setattr(torch.Tensor, "record_stream", lambda self, s: None)
@@ -183,12 +186,17 @@ def test_vecenv_logging_interval_counted_where_it_fires(monkeypatch):
     env.async_reset()
     got = []
     for t in range(1, 7):                       # env-steps 1..6: the interval fires at 3 and 6
-        for _ in range(env.num_batches):
+        for k in range(env.num_batches):
             o, r, d, tr, infos, ids, m = env.recv()
-            got.append((t, len(infos)))
+            got.append((t, k, len(infos)))
             env.send(torch.zeros(64, dtype=torch.uint8))
         assert env.logs_fired == t // 3
-    # records handed out: by the first recv after the interval's last send (env-step 4's), not at 6
-    assert [t for t, k in got if k] == [4]
+    # records handed out: by env-step 4's second recv (its sub-batch was the last stepped at 3)
+    assert [(t, k) for t, k, n in got if n] == [(4, 1)]
+    assert got[-1][2] == 0
+    o, r, d, tr, infos, ids, m = env.recv()
+    assert len(infos) == 0
+    env.send(torch.zeros(64, dtype=torch.uint8))
     o, r, d, tr, infos, ids, m = env.recv()
     assert len(infos) == 1                     # the interval that fired at env-step 6
+    assert infos[0]["episodes"] == 0 and infos[0]["steps"] == 3 * 128
