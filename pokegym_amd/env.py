@@ -424,6 +424,11 @@ class VecEnv:
             actions = torch.from_numpy(actions)
         a = actions.to(device=self.device, dtype=torch.uint8).contiguous()
         self._join_streams()
+        # an interval that fired on a send() and has not been read by a recv() yet
+        pending = []
+        if self._log_wait:
+            self._log_wait = 0
+            pending = self._read_logs()
         if self.num_batches == 1:
             obs, rewards, terminals, truncations = self._step_range(0, a)
         else:
@@ -434,7 +439,7 @@ class VecEnv:
             truncations = torch.cat([o[3] for o in outs])
         self.t += 1
         self._batch_steps += self.num_batches
-        return obs, rewards, terminals, truncations, self._log()
+        return obs, rewards, terminals, truncations, pending + self._log()
 
     def save_state(self, env: int) -> bytes:
         """PyBoy v9 savestate of one env (pk_snapshot; environment.py:208-213 per env)."""

@@ -200,3 +200,21 @@ def test_vecenv_logging_interval_counted_where_it_fires(monkeypatch):
     o, r, d, tr, infos, ids, m = env.recv()
     assert len(infos) == 1                     # the interval that fired at env-step 6
     assert infos[0]["episodes"] == 0 and infos[0]["steps"] == 3 * 128
+
+
+def test_vecenv_step_after_send_reads_the_pending_interval(monkeypatch):
+    """An interval that fired on a send() is handed out by step() if the caller switches from
+    recv/send to step() before the deferred read (VecEnv._read_logs)."""
+    for name in ("Stream", "Event", "current_stream", "stream"):
+        monkeypatch.setattr(torch.cuda, name, _NoStream)
+    monkeypatch.setattr(torch.Tensor, "record_stream", lambda self, s: None)
+    emu = FakeRangeEmu(128, done_every=1000)
+    env = VecEnv(128, emulator=emu, batch_size=64, log_interval=1)
+    env.async_reset()
+    for _ in range(env.num_batches):
+        env.recv()
+        env.send(torch.zeros(64, dtype=torch.uint8))
+    assert env.logs_fired == 1
+    obs, r, d, t, infos = env.step(torch.zeros(128, dtype=torch.uint8))
+    # the pending interval (env-step 1) and the one step() fires itself (env-step 2)
+    assert len(infos) == 2 and infos[0]["steps"] == 128 and infos[1]["steps"] == 128
