@@ -17,16 +17,10 @@
 // ---------------------------------------------------------------------------------------------
 // K2: rasterise the latched lines of the rendered frame.  One wave = one (group, scanline),
 // lane = env: the 64 lanes read the same VRAM offsets of their interleaved images (coalesced).
-// PK_K2_WAVES waves per workgroup (consecutive scanlines of one group: 144 is a multiple of 4),
-// so a launch dispatches a quarter as many workgroups as it has waves.
-#ifndef PK_K2_WAVES
-#define PK_K2_WAVES 4u
-#endif
-__global__ void __launch_bounds__(64 * PK_K2_WAVES) pk_render_kernel(PkStepArgs A) {
-    const u32 line = blockIdx.x * PK_K2_WAVES + (threadIdx.x >> 6);
-    const u32 y = line % PK_ROWS;
-    const u32 gid = A.env0 / PK_LANES + line / PK_ROWS;
-    const u32 lane = threadIdx.x & (PK_LANES - 1u);
+__global__ void __launch_bounds__(64) pk_render_kernel(PkStepArgs A) {
+    const u32 y = blockIdx.x % PK_ROWS;
+    const u32 gid = A.env0 / PK_LANES + blockIdx.x / PK_ROWS;
+    const u32 lane = threadIdx.x;
     const u32 env = gid * PK_LANES + lane;
     if (env >= A.env1) return;
     const u32 rf = A.regs[PK_R_RFLAGS * A.npad + env];
@@ -130,9 +124,8 @@ __global__ void pk_scatter_env_kernel(u8* mem, u32 env, u32 sh, const u8* in) {
 // ---------------------------------------------------------------------------------------------
 // host-side launchers (called by the C ABI in pk_capi.cpp)
 hipError_t pk_launch_render(const PkStepArgs& a, hipStream_t s) {
-    static_assert(PK_ROWS % PK_K2_WAVES == 0, "a K2 workgroup's scanlines stay in one group");
-    const u32 grid = ((a.env1 - a.env0 + PK_LANES - 1u) / PK_LANES) * (PK_ROWS / PK_K2_WAVES);
-    hipLaunchKernelGGL(pk_render_kernel, dim3(grid), dim3(PK_LANES * PK_K2_WAVES), 0, s, a);
+    const u32 grid = ((a.env1 - a.env0 + PK_LANES - 1u) / PK_LANES) * PK_ROWS;
+    hipLaunchKernelGGL(pk_render_kernel, dim3(grid), dim3(PK_LANES), 0, s, a);
     return hipGetLastError();
 }
 
